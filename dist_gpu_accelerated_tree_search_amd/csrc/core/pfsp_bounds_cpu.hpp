@@ -1,0 +1,138 @@
+// Host (CPU) implementations of the three PFSP lower bounds.
+//
+// Parity (same values, same early-exit semantics):
+//   LB1    one-machine bound, full recompute per child   ref c_bound_simple.c:52-158
+//   LB1_d  all children of a parent from one prefix      ref c_bound_simple.c:160-244
+//   LB2    two-machine Johnson bound with early exit      ref c_bound_johnson.c:180-254
+// They serve Step 1 (BFS warm-up), Step 3 (CPU tail), the CPU-only drivers and the
+// CPU workers (-C 1), and are the oracle every GPU kernel is tested against.
+#pragma once
+
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <vector>
+
+#include "pfsp_instance.hpp"
+
+namespace tts {
+
+// Completion times on each machine of the scheduled prefix perm[0..len).
+// An empty prefix uses the per-machine minimum heads (ref schedule_front, limit1==-1).
+template <typename Id>
+inline void cpu_front(const PfspInstance& in, const Id* perm, int len, int* front) {
+  const int N = in.jobs, M = in.machines;
+  if (len == 0) {
+    for (int k = 0; k < M; ++k) front[k] = in.min_heads[k];
+    return;
+  }
+  for (int k = 0; k < M; ++k) front[k] = 0;
+  for (int i = 0; i < len; ++i) {
+    const int j = perm[i];
+    front[0] += in.p[j];
+    for (int k = 1; k < M; ++k) front[k] = std::max(front[k - 1], front[k]) + in.p[static_cast<size_t>(k) * N + j];
+  }
+}
+
+// Sum of processing times of perm[from..N) on each machine.
+template <typename Id>
+inline void cpu_remain(const PfspInstance& in, const Id* perm, int from, int* remain) {
+  const int N = in.jobs, M = in.machines;
+  for (int k = 0; k < M; ++k) remain[k] = 0;
+  for (int i = from; i < N; ++i) {
+    const int j = perm[i];
+    for (int k = 0; k < M; ++k) remain[k] += in.p[static_cast<size_t>(k) * N + j];
+  }
+}
+
+// max over machines of (running max of front+remain) + back; ref machine_bound_from_parts.
+inline int cpu_machine_bound(const int* front, const int* back, const int* remain, int M) {
+  int run = front[0] + remain[0];
+  int lb = run + back[0];
+  for (int k = 1; k < M; ++k) {
+    run = std::max(run, front[k] + remain[k]);
+    lb = std::max(lb, run + back[k]);
+  }
+  return lb;
+}
+
+// LB1 of a node whose scheduled prefix is perm[0..len) (len = limit1+1).
+template <typename Id>
+inline int cpu_lb1(const PfspInstance& in, const Id* perm, int len) {
+  int front[64], remain[64];
+  cpu_front(in, perm, len, front);
+  cpu_remain(in, perm, len, remain);
+  return cpu_machine_bound(front, in.min_tails.data(), remain, in.machines);
+}
+
+// LB1_d: bounds of every child of a parent with prefix perm[0..len).
+// lb_by_job[job] receives the bound of the child that appends `job`.
+template <typename Id>
+inline void cpu_lb1_children(const PfspInstance& in, const Id* perm, int len, int* lb_by_job) {
+  const int N = in.jobs, M = in.machines;
+  int front[64], remain[64];
+  cpu_front(in, perm, len, front);
+  cpu_remain(in, perm, len, remain);
+  const int* back = in.min_tails.data();
+  for (int i = len; i < N; ++i) {
+    const int j = perm[i];
+    // s is the child's start on machine k, and the parent's remain still holds
+    // p[k][j], so s + remain[k] == front'(k) + remain'(k) of the child
+    // (ref add_front_and_bound, c_bound_simple.c:219-244).
+    int lb = front[0] + remain[0] + back[0];
+    int t = front[0] + in.p[j];
+    for (int k = 1; k < M; ++k) {
+      const int s = std::max(t, front[k]);
+      lb = std::max(lb, s + remain[k] + back[k]);
+      t = s + in.p[static_cast<size_t>(k) * N + j];
+    }
+    lb_by_job[j] = lb;
+  }
+}
+
+// LB2 of a node with prefix perm[0..len); stops once the partial max exceeds `best`
+// (the returned value is then only guaranteed to be > best).
+template <typename Id>
+inline int cpu_lb2(const PfspInstance& in, const Id* perm, int len, int best) {
+  const int N = in.jobs, M = in.machines;
+  int front[64];
+  cpu_front(in, perm, len, front);
+  const int* back = in.min_tails.data();
+  // scheduled flags
+  uint8_t sched[512];
+  for (int j = 0; j < N; ++j) sched[j] = 0;
+  for (int i = 0; i < len; ++i) sched[perm[i]] = 1;
+  (void)M;
+  int lb = 0;
+  for (int q = 0; q < in.npairs; ++q) {
+    const int m0 = in.pair_m0[q], m1 = in.pair_m1[q];
+    int t0 = front[m0], t1 = front[m1];
+    const int* order = &in.johnson[static_cast<size_t>(q) * N];
+    const int* lag = &in.lags[static_cast<size_t>(q) * N];
+    for (int r = 0; r < N; ++r) {
+      const int j = order[r];
+      if (sched[j]) continue;
+      t0 += in.p[static_cast<size_t>(m0) * N + j];
+      t1 = std::max(t1, t0 + lag[j]) + in.p[static_cast<size_t>(m1) * N + j];
+    }
+    lb = std::max(lb, std::max(t1 + back[m1], t0 + back[m0]));
+    if (lb > best) break;
+  }
+  return lb;
+}
+
+// Makespan of a complete permutation (used by tests as the ground truth).
+template <typename Id>
+inline int cpu_makespan(const PfspInstance& in, const Id* perm) {
+  int front[64];
+  const int N = in.jobs, M = in.machines;
+  for (int k = 0; k < M; ++k) front[k] = 0;
+  for (int i = 0; i < N; ++i) {
+    const int j = perm[i];
+    front[0] += in.p[j];
+    for (int k = 1; k < M; ++k) front[k] = std::max(front[k - 1], front[k]) + in.p[static_cast<size_t>(k) * N + j];
+  }
+  return front[M - 1];
+}
+
+}  // namespace tts
