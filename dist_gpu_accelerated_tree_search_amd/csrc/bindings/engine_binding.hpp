@@ -1,0 +1,79 @@
+// pybind11 class for the engine contract (csrc/core/engine_api.hpp), shared by the
+// CPU module (_tts_cpu) and the HIP module (_tts_hip). Nodes cross the boundary as
+// uint8 arrays of shape (n, node_bytes) in the exact device layout.
+#pragma once
+
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+
+#include <memory>
+#include <stdexcept>
+
+#include "../core/engine_api.hpp"
+
+namespace py = pybind11;
+
+namespace tts {
+
+inline py::dict engine_stats_dict(const EngineStats& s) {
+  py::dict d;
+  d["tree"] = s.tree;
+  d["sol"] = s.sol;
+  d["parents"] = s.parents;
+  d["iters"] = s.iters;
+  d["best"] = s.best;
+  d["launches"] = s.launches;
+  d["syncs"] = s.syncs;
+  d["spilled"] = s.spilled;
+  d["refilled"] = s.refilled;
+  d["t_run"] = s.t_run;
+  d["t_memcpy"] = s.t_memcpy;
+  d["t_malloc"] = s.t_malloc;
+  d["device_nodes"] = s.device_nodes;
+  d["host_nodes"] = s.host_nodes;
+  d["capacity"] = s.capacity;
+  return d;
+}
+
+inline void bind_engine(py::module_& m) {
+  using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+  py::class_<IEngine, std::unique_ptr<IEngine>>(m, "Engine", py::module_local())
+      .def_property_readonly("node_bytes", &IEngine::node_bytes)
+      .def_property_readonly("device", &IEngine::device)
+      .def_property_readonly("stream", &IEngine::stream)
+      .def(
+          "push",
+          [](IEngine& e, U8 a) {
+            if (a.ndim() != 2 || static_cast<size_t>(a.shape(1)) != e.node_bytes())
+              throw std::invalid_argument("nodes must be a (n, node_bytes) uint8 array");
+            e.push_host(a.data(), static_cast<size_t>(a.shape(0)));
+          },
+          "Push nodes (top of the pool).")
+      .def(
+          "pop",
+          [](IEngine& e, size_t max_n) {
+            U8 out({static_cast<py::ssize_t>(max_n), static_cast<py::ssize_t>(e.node_bytes())});
+            const size_t n = e.pop_host(out.mutable_data(), max_n);
+            return py::array(out[py::slice(0, static_cast<py::ssize_t>(n), 1)]);
+          },
+          py::arg("max_n"), "Remove up to max_n nodes (oldest first) to a host array.")
+      .def(
+          "export_to",
+          [](IEngine& e, uintptr_t ptr, size_t max_n) { return e.export_device(reinterpret_cast<void*>(ptr), max_n); },
+          py::arg("ptr"), py::arg("max_n"), py::call_guard<py::gil_scoped_release>(),
+          "Move up to max_n oldest nodes into device memory at ptr (same device); returns the count.")
+      .def(
+          "import_from",
+          [](IEngine& e, uintptr_t ptr, size_t n) { e.import_device(reinterpret_cast<const void*>(ptr), n); },
+          py::arg("ptr"), py::arg("n"), py::call_guard<py::gil_scoped_release>(),
+          "Append n nodes read from device memory at ptr.")
+      .def("size", &IEngine::size, py::call_guard<py::gil_scoped_release>())
+      .def("run", &IEngine::run, py::arg("max_launches") = -1, py::arg("max_seconds") = 0.0,
+           py::arg("stop_below") = 0, py::call_guard<py::gil_scoped_release>())
+      .def_property("best", &IEngine::best, &IEngine::set_best)
+      .def("reset_counters", &IEngine::reset_counters)
+      .def("stats", [](IEngine& e) { return engine_stats_dict(e.stats()); })
+      .def("synchronize", &IEngine::synchronize, py::call_guard<py::gil_scoped_release>());
+}
+
+}  // namespace tts

@@ -1,0 +1,233 @@
+// _tts_cpu: host-side native core (no HIP dependency; builds and runs anywhere).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <climits>
+
+#include "../core/cpu_engine.hpp"
+#include "../core/drivers_cpu.hpp"
+#include "engine_binding.hpp"
+
+namespace py = pybind11;
+using namespace tts;
+
+namespace {
+
+using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+
+template <class Node>
+U8 nodes_to_array(const Node* p, size_t n) {
+  U8 out({static_cast<py::ssize_t>(n), static_cast<py::ssize_t>(sizeof(Node))});
+  if (n) std::memcpy(out.mutable_data(), p, n * sizeof(Node));
+  return out;
+}
+
+template <class Node>
+const Node* array_nodes(const U8& a, size_t& n) {
+  if (a.ndim() != 2 || static_cast<size_t>(a.shape(1)) != sizeof(Node))
+    throw std::invalid_argument("nodes must be a (n, node_bytes) uint8 array");
+  n = static_cast<size_t>(a.shape(0));
+  return reinterpret_cast<const Node*>(a.data());
+}
+
+py::dict worker_dict(const WorkerStats& w) {
+  py::dict d;
+  d["tree"] = w.tree;
+  d["sol"] = w.sol;
+  d["gen_child"] = w.gen_child;
+  d["steals"] = w.steals;
+  d["success_steals"] = w.success_steals;
+  d["terminations"] = w.terminations;
+  d["t_memcpy"] = w.t_memcpy;
+  d["t_malloc"] = w.t_malloc;
+  d["t_kernel"] = w.t_kernel;
+  d["t_gen_child"] = w.t_gen_child;
+  d["t_pool_ops"] = w.t_pool_ops;
+  d["t_idle"] = w.t_idle;
+  d["t_termination"] = w.t_termination;
+  return d;
+}
+
+py::dict result_dict(const RunResult& r) {
+  py::dict d;
+  d["best"] = r.best;
+  d["tree"] = r.tree;
+  d["sol"] = r.sol;
+  d["t_init"] = r.t_init;
+  d["t_search"] = r.t_search;
+  d["t_tail"] = r.t_tail;
+  d["elapsed"] = r.elapsed;
+  py::list ws;
+  for (auto& w : r.workers) ws.append(worker_dict(w));
+  d["workers"] = ws;
+  return d;
+}
+
+MulticoreConfig mc_config(size_t m, size_t batch, size_t steal_cap, bool ws) {
+  MulticoreConfig c;
+  c.m = m;
+  c.batch = batch;
+  c.steal_cap = steal_cap;
+  c.work_stealing = ws;
+  return c;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_tts_cpu, m) {
+  m.doc() = "Native host core of the MI355X tree-search engine (Taillard, bounds, pools, CPU drivers).";
+  bind_engine(m);
+
+  // ---- Taillard ----
+  m.def("taillard_jobs", &taillard_jobs);
+  m.def("taillard_machines", &taillard_machines);
+  m.def("taillard_best_ub", &taillard_best_ub);
+  m.def("taillard_processing_times", &taillard_processing_times, "machine-major p[m*N+j]");
+  m.def("synthetic_processing_times", &synthetic_processing_times, py::arg("jobs"), py::arg("machines"),
+        py::arg("seed"));
+
+  py::class_<PfspInstance>(m, "PfspInstance")
+      .def_static("taillard", &make_taillard_instance, py::arg("id"))
+      .def_static(
+          "from_matrix",
+          [](int jobs, int machines, std::vector<int> p, int best_known) {
+            return make_instance(jobs, machines, std::move(p), 0, best_known);
+          },
+          py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("best_known") = INT_MAX)
+      .def_readonly("id", &PfspInstance::id)
+      .def_readonly("jobs", &PfspInstance::jobs)
+      .def_readonly("machines", &PfspInstance::machines)
+      .def_readonly("best_known", &PfspInstance::best_known)
+      .def_readonly("p", &PfspInstance::p)
+      .def_readonly("min_heads", &PfspInstance::min_heads)
+      .def_readonly("min_tails", &PfspInstance::min_tails)
+      .def_readonly("npairs", &PfspInstance::npairs)
+      .def_readonly("pair_m0", &PfspInstance::pair_m0)
+      .def_readonly("pair_m1", &PfspInstance::pair_m1)
+      .def_readonly("lags", &PfspInstance::lags)
+      .def_readonly("johnson", &PfspInstance::johnson);
+
+  // ---- bounds (oracle for the GPU kernels) ----
+  m.def("lb1", [](const PfspInstance& in, std::vector<int> prmu, int len) { return cpu_lb1(in, prmu.data(), len); });
+  m.def("lb1_children", [](const PfspInstance& in, std::vector<int> prmu, int len) {
+    std::vector<int> out(in.jobs, 0);
+    cpu_lb1_children(in, prmu.data(), len, out.data());
+    return out;
+  });
+  m.def("lb2", [](const PfspInstance& in, std::vector<int> prmu, int len, int best) {
+    return cpu_lb2(in, prmu.data(), len, best);
+  });
+  m.def("makespan", [](const PfspInstance& in, std::vector<int> perm) { return cpu_makespan(in, perm.data()); });
+
+  m.def("pfsp_node_bytes", [](int jobs) {
+    return with_pfsp_bucket(jobs, [](auto nj) { return sizeof(PfspNode<decltype(nj)::value>); });
+  });
+  m.def("pfsp_bucket", &pfsp_bucket);
+  m.def("queens_node_bytes", []() { return sizeof(QueensNode); });
+
+  // ---- end-to-end CPU drivers ----
+  m.def(
+      "run_pfsp",
+      [](const PfspInstance& in, int lb, int best, int threads, size_t m_, size_t batch, size_t steal_cap, bool ws,
+         bool verbose) {
+        py::gil_scoped_release nogil;
+        RunResult r = run_pfsp_cpu(in, lb, best, threads, mc_config(m_, batch, steal_cap, ws), verbose);
+        py::gil_scoped_acquire gil;
+        return result_dict(r);
+      },
+      py::arg("inst"), py::arg("lb"), py::arg("best"), py::arg("threads") = 0, py::arg("m") = 25,
+      py::arg("batch") = 20000, py::arg("steal_cap") = 250000, py::arg("ws") = true, py::arg("verbose") = false);
+  m.def(
+      "run_queens",
+      [](int N, int G, int threads, size_t m_, size_t batch, size_t steal_cap, bool ws, bool verbose) {
+        py::gil_scoped_release nogil;
+        RunResult r = run_queens_cpu(N, G, threads, mc_config(m_, batch, steal_cap, ws), verbose);
+        py::gil_scoped_acquire gil;
+        return result_dict(r);
+      },
+      py::arg("N"), py::arg("G") = 1, py::arg("threads") = 0, py::arg("m") = 25, py::arg("batch") = 20000,
+      py::arg("steal_cap") = 250000, py::arg("ws") = true, py::arg("verbose") = false);
+
+  // ---- Step 1 (BFS warm-up) and Step 3 (DFS drain) for the GPU/distributed drivers ----
+  m.def(
+      "pfsp_bfs",
+      [](const PfspInstance& in, int lb, int best, size_t target) {
+        return with_pfsp_bucket(in.jobs, [&](auto nj) {
+          constexpr int NJ = decltype(nj)::value;
+          PfspProblem<NJ> prob(in, lb);
+          Pool<PfspNode<NJ>> pool;
+          pool.push_back_free(prob.root());
+          u64 tree = 0, sol = 0;
+          bfs_warmup(prob, pool, target, best, tree, sol);
+          return py::make_tuple(nodes_to_array(pool.data(), pool.size()), tree, sol, best);
+        });
+      },
+      py::arg("inst"), py::arg("lb"), py::arg("best"), py::arg("target"));
+  m.def(
+      "pfsp_drain",
+      [](const PfspInstance& in, int lb, int best, U8 nodes) {
+        return with_pfsp_bucket(in.jobs, [&](auto nj) {
+          constexpr int NJ = decltype(nj)::value;
+          using Node = PfspNode<NJ>;
+          PfspProblem<NJ> prob(in, lb);
+          size_t n = 0;
+          const Node* p = array_nodes<Node>(nodes, n);
+          Pool<Node> pool;
+          pool.push_back_bulk_free(p, n);
+          u64 tree = 0, sol = 0;
+          {
+            py::gil_scoped_release nogil;
+            dfs_drain(prob, pool, best, tree, sol);
+          }
+          return py::make_tuple(tree, sol, best);
+        });
+      },
+      py::arg("inst"), py::arg("lb"), py::arg("best"), py::arg("nodes"));
+  m.def(
+      "queens_bfs",
+      [](int N, int G, size_t target) {
+        QueensProblem prob(N, G);
+        Pool<QueensNode> pool;
+        pool.push_back_free(prob.root());
+        u64 tree = 0, sol = 0;
+        int best = 0;
+        bfs_warmup(prob, pool, target, best, tree, sol);
+        return py::make_tuple(nodes_to_array(pool.data(), pool.size()), tree, sol);
+      },
+      py::arg("N"), py::arg("G"), py::arg("target"));
+  m.def(
+      "queens_drain",
+      [](int N, int G, U8 nodes) {
+        QueensProblem prob(N, G);
+        size_t n = 0;
+        const QueensNode* p = array_nodes<QueensNode>(nodes, n);
+        Pool<QueensNode> pool;
+        pool.push_back_bulk_free(p, n);
+        u64 tree = 0, sol = 0;
+        int best = 0;
+        {
+          py::gil_scoped_release nogil;
+          dfs_drain(prob, pool, best, tree, sol);
+        }
+        return py::make_tuple(tree, sol);
+      },
+      py::arg("N"), py::arg("G"), py::arg("nodes"));
+
+  // ---- CPU engines (same contract as the GPU engines) ----
+  m.def(
+      "make_pfsp_cpu_engine",
+      [](const PfspInstance& in, int lb, size_t batch, int threads) -> std::unique_ptr<IEngine> {
+        return with_pfsp_bucket(in.jobs, [&](auto nj) -> std::unique_ptr<IEngine> {
+          constexpr int NJ = decltype(nj)::value;
+          return std::make_unique<CpuEngine<PfspProblem<NJ>>>(PfspProblem<NJ>(in, lb), batch, threads);
+        });
+      },
+      py::arg("inst"), py::arg("lb"), py::arg("batch") = 4096, py::arg("threads") = 1, py::keep_alive<0, 1>());
+  m.def(
+      "make_queens_cpu_engine",
+      [](int N, int G, size_t batch, int threads) -> std::unique_ptr<IEngine> {
+        return std::make_unique<CpuEngine<QueensProblem>>(QueensProblem(N, G), batch, threads);
+      },
+      py::arg("N"), py::arg("G") = 1, py::arg("batch") = 4096, py::arg("threads") = 1);
+}

@@ -1,0 +1,120 @@
+// _tts_hip: gfx950 device engines and kernels. Instances are passed as plain
+// (jobs, machines, machine-major p) data so this module shares no C++ types with
+// _tts_cpu (the two are built by different compilers).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <climits>
+#include <string>
+
+#include "../hip/pfsp_engine.hpp"
+#include "../hip/queens_engine.hpp"
+#include "engine_binding.hpp"
+
+namespace py = pybind11;
+using namespace tts;
+
+namespace {
+
+using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+
+EngineConfig make_cfg(int device, size_t max_parents, size_t ring_bytes, int iters_small, int iters_large,
+                      bool use_graphs, uintptr_t stream) {
+  EngineConfig c;
+  c.device = device;
+  c.max_parents = max_parents;
+  c.ring_bytes = ring_bytes;
+  c.iters_small = iters_small;
+  c.iters_large = iters_large;
+  c.use_graphs = use_graphs;
+  c.external_stream = stream;
+  return c;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_tts_hip, m) {
+  m.doc() = "gfx950 (MI355X) device engines: device-resident pools, fused bound/prune/compact kernels, hipGraphs.";
+  bind_engine(m);
+
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("device_info", [](int device) {
+    hipDeviceProp_t p;
+    TTS_HIP_CHECK(hipGetDeviceProperties(&p, device));
+    py::dict d;
+    d["name"] = std::string(p.name);
+    d["arch"] = std::string(p.gcnArchName);
+    d["compute_units"] = p.multiProcessorCount;
+    d["clock_khz"] = p.clockRate;
+    d["total_mem"] = static_cast<size_t>(p.totalGlobalMem);
+    d["lds_per_block"] = static_cast<size_t>(p.sharedMemPerBlock);
+    d["warp_size"] = p.warpSize;
+    return d;
+  });
+
+  m.def(
+      "make_pfsp_engine",
+      [](int jobs, int machines, std::vector<int> p, int lb, int device, size_t max_parents, size_t ring_bytes,
+         int iters_small, int iters_large, bool use_graphs, uintptr_t stream, int taillard_id) {
+        const PfspInstance in = make_instance(jobs, machines, std::move(p), taillard_id);
+        py::gil_scoped_release nogil;
+        return make_pfsp_engine(in, lb,
+                                make_cfg(device, max_parents, ring_bytes, iters_small, iters_large, use_graphs, stream));
+      },
+      py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("device") = 0,
+      py::arg("max_parents") = size_t(1) << 18, py::arg("ring_bytes") = size_t(16) << 30, py::arg("iters_small") = 6,
+      py::arg("iters_large") = 48, py::arg("use_graphs") = true, py::arg("stream") = 0, py::arg("taillard_id") = 0);
+
+  m.def(
+      "make_queens_engine",
+      [](int N, int G, int device, size_t max_parents, size_t ring_bytes, int iters_small, int iters_large,
+         bool use_graphs, uintptr_t stream) {
+        py::gil_scoped_release nogil;
+        return make_queens_engine(
+            N, G, make_cfg(device, max_parents, ring_bytes, iters_small, iters_large, use_graphs, stream));
+      },
+      py::arg("N"), py::arg("G") = 1, py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 20,
+      py::arg("ring_bytes") = size_t(16) << 30, py::arg("iters_small") = 6, py::arg("iters_large") = 48,
+      py::arg("use_graphs") = true, py::arg("stream") = 0);
+
+  m.def(
+      "pfsp_bounds",
+      [](int jobs, int machines, std::vector<int> p, int lb, U8 parents, int best, int device) {
+        const PfspInstance in = make_instance(jobs, machines, std::move(p));
+        const size_t nb = with_pfsp_bucket(jobs, [](auto nj) { return sizeof(PfspNode<decltype(nj)::value>); });
+        if (parents.ndim() != 2 || static_cast<size_t>(parents.shape(1)) != nb)
+          throw std::invalid_argument("parents must be a (n, node_bytes) uint8 array");
+        std::vector<int> out;
+        {
+          py::gil_scoped_release nogil;
+          out = pfsp_gpu_bounds(in, lb, parents.data(), static_cast<size_t>(parents.shape(0)), best, device);
+        }
+        py::array_t<int> r(static_cast<py::ssize_t>(out.size()));
+        std::memcpy(r.mutable_data(), out.data(), out.size() * sizeof(int));
+        return r;
+      },
+      py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("parents"), py::arg("best") = INT_MAX,
+      py::arg("device") = 0);
+
+  m.def(
+      "queens_labels",
+      [](int N, int G, U8 parents, int device) {
+        if (parents.ndim() != 2 || parents.shape(1) != static_cast<py::ssize_t>(sizeof(QueensNode)))
+          throw std::invalid_argument("parents must be a (n, 16) uint8 array");
+        const size_t n = static_cast<size_t>(parents.shape(0));
+        std::vector<uint8_t> out;
+        {
+          py::gil_scoped_release nogil;
+          out = queens_gpu_labels(N, G, reinterpret_cast<const QueensNode*>(parents.data()), n, device);
+        }
+        U8 r({static_cast<py::ssize_t>(n), static_cast<py::ssize_t>(N)});
+        std::memcpy(r.mutable_data(), out.data(), out.size());
+        return r;
+      },
+      py::arg("N"), py::arg("G"), py::arg("parents"), py::arg("device") = 0);
+}

@@ -1,0 +1,122 @@
+// Host (CPU) implementation of the engine contract of csrc/hip/engine.hpp.
+//
+// It lets the distributed runtime (parallel/) and its termination / work-sharing
+// logic run unchanged on CPU-only machines over the gloo backend (the reference has
+// no loopback harness at all), and it is the CPU worker used next to
+// the GPUs for -C 1. "Device" pointers are host pointers here.
+#pragma once
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "engine_api.hpp"
+#include "search_cpu.hpp"
+
+namespace tts {
+
+template <class Problem>
+class CpuEngine final : public IEngine {
+ public:
+  using Node = typename Problem::Node;
+
+  CpuEngine(Problem prob, size_t batch, int threads) : prob_(std::move(prob)), batch_(std::max<size_t>(1, batch)),
+                                                        threads_(std::max(1, threads)) {}
+
+  size_t node_bytes() const override { return sizeof(Node); }
+  size_t size() override { return pool_.size(); }
+  int best() override { return best_; }
+  void set_best(int b) override { best_ = b; }
+  void reset_counters() override { tree_ = sol_ = parents_ = launches_ = 0; }
+  void synchronize() override {}
+  uintptr_t stream() const override { return 0; }
+  int device() const override { return -1; }
+
+  void push_host(const void* nodes, size_t n) override {
+    pool_.push_back_bulk_free(static_cast<const Node*>(nodes), n);
+  }
+  void import_device(const void* src, size_t n) override { push_host(src, n); }
+
+  // Oldest (bottom) nodes first, like the GPU engine's export.
+  size_t pop_host(void* out, size_t max_n) override {
+    const size_t n = std::min(max_n, pool_.size());
+    Node tmp;
+    Node* dst = static_cast<Node*>(out);
+    for (size_t i = 0; i < n; ++i) {
+      pool_.pop_front_free(tmp);
+      dst[i] = tmp;
+    }
+    return n;
+  }
+  size_t export_device(void* dst, size_t max_n) override { return pop_host(dst, max_n); }
+
+  // One "launch" expands up to `batch` parents from the top of the pool.
+  long run(long max_launches, double max_seconds, size_t stop_below) override {
+    const double t0 = now_s();
+    long launches = 0;
+    std::vector<Node> parents(batch_);
+    while (!pool_.empty() && pool_.size() >= std::max<size_t>(stop_below, 1)) {
+      if (max_launches >= 0 && launches >= max_launches) break;
+      if (max_seconds > 0 && now_s() - t0 >= max_seconds) break;
+      const size_t n = pool_.pop_back_bulk_free(1, batch_, parents.data(), 1);
+      expand(parents.data(), n);
+      parents_ += n;
+      ++launches;
+    }
+    launches_ += launches;
+    t_run_ += now_s() - t0;
+    return launches;
+  }
+
+  EngineStats stats() override {
+    EngineStats s;
+    s.tree = tree_;
+    s.sol = sol_;
+    s.parents = parents_;
+    s.iters = launches_;
+    s.launches = launches_;
+    s.best = best_;
+    s.device_nodes = pool_.size();
+    s.t_run = t_run_;
+    return s;
+  }
+
+ private:
+  void expand(const Node* parents, size_t n) {
+    if (threads_ == 1 || n < 256) {
+      for (size_t i = 0; i < n; ++i)
+        prob_.decompose(parents[i], best_, tree_, sol_, [&](const Node& c) { pool_.push_back_free(c); });
+      return;
+    }
+    // static split of the batch over threads, children merged afterwards
+    std::vector<std::vector<Node>> out(threads_);
+    std::vector<u64> tr(threads_, 0), so(threads_, 0);
+    std::vector<int> bl(threads_, best_);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads_; ++t)
+      th.emplace_back([&, t]() {
+        for (size_t i = t; i < n; i += threads_)
+          prob_.decompose(parents[i], bl[t], tr[t], so[t], [&](const Node& c) { out[t].push_back(c); });
+      });
+    for (auto& x : th) x.join();
+    for (int t = 0; t < threads_; ++t) {
+      tree_ += tr[t];
+      sol_ += so[t];
+      best_ = std::min(best_, bl[t]);
+      pool_.push_back_bulk_free(out[t].data(), out[t].size());
+    }
+  }
+
+  Problem prob_;
+  size_t batch_;
+  int threads_;
+  Pool<Node> pool_;
+  int best_ = 0x7fffffff;
+  u64 tree_ = 0, sol_ = 0, parents_ = 0, launches_ = 0;
+  double t_run_ = 0;
+};
+
+}  // namespace tts

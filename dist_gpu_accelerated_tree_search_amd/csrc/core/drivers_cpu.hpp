@@ -22,17 +22,6 @@ struct RunResult {
   std::vector<WorkerStats> workers;
 };
 
-template <class F>
-decltype(auto) with_pfsp_bucket(int jobs, F&& f) {
-  switch (pfsp_bucket(jobs)) {
-    case 20: return f(std::integral_constant<int, 20>{});
-    case 50: return f(std::integral_constant<int, 50>{});
-    case 100: return f(std::integral_constant<int, 100>{});
-    case 200: return f(std::integral_constant<int, 200>{});
-    default: return f(std::integral_constant<int, 500>{});
-  }
-}
-
 template <class Problem>
 RunResult run_sequential(const Problem& prob, int best_init) {
   using Node = typename Problem::Node;

@@ -1,0 +1,52 @@
+// Engine contract shared by the GPU engine (csrc/hip/engine.hpp) and the CPU engine
+// (csrc/core/cpu_engine.hpp), so the Python runtime and the distributed protocol
+// (parallel/) drive either one through the same calls.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+namespace tts {
+
+struct EngineConfig {
+  int device = 0;
+  size_t max_parents = size_t(1) << 18;  // parents expanded per iteration (reference -M)
+  size_t ring_bytes = size_t(16) << 30;  // device ring capacity in bytes (rounded down to 2^k nodes)
+  int iters_small = 6;                   // iterations per small graph (multiple of 6)
+  int iters_large = 48;                  // iterations per large graph (multiple of 6)
+  bool use_graphs = true;
+  uintptr_t external_stream = 0;         // run on this stream when non-zero
+};
+
+struct EngineStats {
+  unsigned long long tree = 0, sol = 0, parents = 0, iters = 0;
+  int best = 0;
+  unsigned long long launches = 0, syncs = 0, spilled = 0, refilled = 0;
+  double t_run = 0, t_memcpy = 0, t_malloc = 0;
+  size_t device_nodes = 0, host_nodes = 0, capacity = 0;
+};
+
+// Type-erased interface used by the Python bindings and the native CLIs.
+class IEngine {
+ public:
+  virtual ~IEngine() = default;
+  virtual size_t node_bytes() const = 0;
+  virtual void push_host(const void* nodes, size_t n) = 0;
+  virtual size_t pop_host(void* out, size_t max_n) = 0;
+  virtual size_t export_device(void* dst, size_t max_n) = 0;
+  virtual void import_device(const void* src, size_t n) = 0;
+  virtual size_t size() = 0;
+  // Replays expand graphs until the pool is empty, `max_launches` graphs were
+  // launched (<0: unlimited), `max_seconds` elapsed (<=0: unlimited), or the pool
+  // dropped below `stop_below` nodes. Returns the number of graph launches.
+  virtual long run(long max_launches, double max_seconds, size_t stop_below) = 0;
+  virtual void set_best(int b) = 0;
+  virtual int best() = 0;
+  virtual void reset_counters() = 0;
+  virtual EngineStats stats() = 0;
+  virtual void synchronize() = 0;
+  virtual uintptr_t stream() const = 0;
+  virtual int device() const = 0;
+};
+
+}  // namespace tts

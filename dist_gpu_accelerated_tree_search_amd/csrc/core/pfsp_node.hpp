@@ -15,6 +15,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <type_traits>
+#include <utility>
 
 #ifndef TTS_HD
 #if defined(__HIPCC__)
@@ -62,6 +63,18 @@ inline int pfsp_bucket(int jobs) {
   if (jobs <= 100) return 100;
   if (jobs <= 200) return 200;
   return 500;
+}
+
+// Calls f(std::integral_constant<int, NJ>{}) for the bucket of `jobs`.
+template <class F>
+decltype(auto) with_pfsp_bucket(int jobs, F&& f) {
+  switch (pfsp_bucket(jobs)) {
+    case 20: return f(std::integral_constant<int, 20>{});
+    case 50: return f(std::integral_constant<int, 50>{});
+    case 100: return f(std::integral_constant<int, 100>{});
+    case 200: return f(std::integral_constant<int, 200>{});
+    default: return f(std::integral_constant<int, 500>{});
+  }
 }
 
 // N-Queens node (ref nqueens/lib/NQueens_node.h:13-17 stores the full board,

@@ -1,0 +1,90 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#define TTS_HIP_CHECK(expr)                                                                          \
+  do {                                                                                               \
+    hipError_t _e = (expr);                                                                          \
+    if (_e != hipSuccess)                                                                            \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + __FILE__ + \
+                               ":" + std::to_string(__LINE__) + " in " #expr);                      \
+  } while (0)
+
+namespace tts {
+namespace dev {
+
+using u64 = unsigned long long;
+
+constexpr int kWave = 64;      // CDNA wavefront width
+constexpr int kBlock = 256;    // 4 waves per workgroup for every search kernel
+
+// Pool control block (device memory). The device-resident pool is
+//   * a ring-buffer stack  ring[(bot + i) & mask], i < stack[s]
+//   * plus the children buffer written by the previous iteration, bufs[t%2][0..buf[s])
+// Iteration t of a launch sequence reads slot t%3, accumulates into slot (t+1)%3 and
+// clears slot (t+2)%3 (the one read by iteration t-1), so consecutive kernels never
+// race on a counter, with no per-iteration host work and no extra launch.
+// Every field that device atomics touch sits on its own 128-B line, apart from the
+// fields that are plain-stored, so a plain write-back never merges with an atomic.
+struct alignas(128) CtlU64 {
+  u64 v;
+  u64 pad[15];
+};
+struct alignas(128) CtlI32 {
+  int v;
+  int pad[31];
+};
+
+struct PoolCtl {
+  CtlU64 buf[3];    // children in buffer (t%2) for state slot s; atomicAdd during an iteration
+  CtlU64 stack[3];  // stack size for state slot s; plain store by workgroup 0
+  CtlU64 tree;      // pushed children (explored tree)
+  CtlU64 sol;       // evaluated leaves (explored solutions)
+  CtlI32 best;      // incumbent (atomicMin by leaves)
+  // plain fields: written by workgroup 0 or by the host between launches
+  u64 bot;          // ring base of the stack
+  u64 parents;      // parents expanded (diagnostics)
+  u64 iters;        // iterations that had work (diagnostics)
+  int overflow;     // set when a ring write would exceed capacity
+  int pad0;
+};
+
+// Workgroup exclusive scan of one int per thread (kBlock threads).
+// `scratch` needs kBlock/kWave ints of LDS. Returns the exclusive prefix; *total
+// receives the block sum. Contains __syncthreads().
+__device__ inline int block_exclusive_scan(int v, int* scratch, int* total) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) scratch[wid] = x;
+  __syncthreads();
+  int wave_off = 0, sum = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) {
+    const int s = scratch[w];
+    wave_off += (w < wid) ? s : 0;
+    sum += s;
+  }
+  *total = sum;
+  __syncthreads();
+  return wave_off + x - v;
+}
+
+__device__ inline u64 lanemask_lt() {
+  const int lane = threadIdx.x & (kWave - 1);
+  return lane == 0 ? 0ull : (~0ull >> (kWave - lane));
+}
+
+}  // namespace dev
+}  // namespace tts

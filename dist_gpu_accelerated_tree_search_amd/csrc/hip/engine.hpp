@@ -1,0 +1,369 @@
+// Host orchestration of one GPU's device-resident B&B pool.
+//
+// Replaces the reference's per-batch host loop (ref pfsp_multigpu_cuda.c:221-332:
+// popBackBulk -> build nodeIndex/sumOffSets on the CPU -> 3 synchronous H2D copies
+// -> kernel -> cudaDeviceSynchronize -> D2H bounds -> generate_children on the CPU
+// -> pushBackBulk) with:
+//   * a ring-buffer stack + ping-pong children buffers in HBM (sized for 288 GB),
+//   * K fused expand iterations captured once into a hipGraph and replayed; the
+//     iteration count, parent window and pool sizes live in device memory
+//     (PoolCtl), so the host only reads a 1-KB control block between replays,
+//   * host spill/refill of the ring bottom when the ring nears capacity, and
+//     bottom export/import for work sharing between GPUs (steal the shallowest,
+//     largest subtrees, RCCL transfer done by the caller: parallel/).
+#pragma once
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <vector>
+
+#include "../core/engine_api.hpp"
+#include "device_common.hpp"
+
+namespace tts {
+
+// Traits contract:
+//   using Node; using Args; static constexpr int kMaxChildren(const Args&);
+//   static void launch(const Args&, int t, int grid, hipStream_t);
+//   static int blocks_per_cu();   static int parents_per_block();
+template <class Traits>
+class DeviceEngine final : public IEngine {
+ public:
+  using Node = typename Traits::Node;
+  using Args = typename Traits::Args;
+
+  DeviceEngine(const EngineConfig& cfg, const Args& problem_args, int max_children) : cfg_(cfg), args_(problem_args) {
+    if (cfg_.iters_small % 6 || cfg_.iters_large % 6 || cfg_.iters_small <= 0 || cfg_.iters_large <= 0)
+      throw std::invalid_argument("iterations per graph must be positive multiples of 6");
+    if (cfg_.max_parents == 0) throw std::invalid_argument("max_parents must be > 0");
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    const auto t0 = std::chrono::steady_clock::now();
+    max_children_ = static_cast<size_t>(max_children);
+    size_t cap = 1;
+    while (cap * 2 * sizeof(Node) <= cfg_.ring_bytes) cap *= 2;
+    const size_t min_cap = cfg_.max_parents * max_children_ * 8;
+    while (cap < min_cap) cap *= 2;
+    cap_ = cap;
+    buf_nodes_ = cfg_.max_parents * max_children_;
+    TTS_HIP_CHECK(hipMalloc(&d_ring_, cap_ * sizeof(Node)));
+    TTS_HIP_CHECK(hipMalloc(&d_buf_[0], buf_nodes_ * sizeof(Node)));
+    TTS_HIP_CHECK(hipMalloc(&d_buf_[1], buf_nodes_ * sizeof(Node)));
+    TTS_HIP_CHECK(hipMalloc(&d_ctl_, sizeof(dev::PoolCtl)));
+    TTS_HIP_CHECK(hipHostMalloc(&h_ctl_, sizeof(dev::PoolCtl), hipHostMallocDefault));
+    std::memset(h_ctl_, 0, sizeof(dev::PoolCtl));
+    h_ctl_->best.v = 0x7fffffff;
+    if (cfg_.external_stream) {
+      stream_ = reinterpret_cast<hipStream_t>(cfg_.external_stream);
+    } else {
+      TTS_HIP_CHECK(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking));
+      stream_ = own_stream_;
+    }
+    args_.stack = d_ring_;
+    args_.buf[0] = d_buf_[0];
+    args_.buf[1] = d_buf_[1];
+    args_.ctl = d_ctl_;
+    args_.cap_mask = cap_ - 1;
+    args_.max_parents = static_cast<int>(cfg_.max_parents);
+    int cus = 0;
+    TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+    const int per_cu = std::max(1, Traits::blocks_per_cu());
+    const size_t want = (cfg_.max_parents + Traits::parents_per_block() - 1) / Traits::parents_per_block();
+    grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, static_cast<size_t>(cus) * per_cu)));
+    upload_ctl();
+    // graphs of 6, 12, 24, ... iterations up to iters_large; run() picks the
+    // largest one whose worst-case ring growth still fits
+    for (int k = cfg_.iters_small; k <= cfg_.iters_large; k *= 2) {
+      ks_.push_back(k);
+      if (cfg_.use_graphs) graphs_.push_back(capture(k));
+    }
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    stats_.t_malloc = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
+  ~DeviceEngine() override {
+    (void)hipSetDevice(cfg_.device);
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto g : graphs_) (void)hipGraphExecDestroy(g);
+    for (void* p : owned_) (void)hipFree(p);
+    (void)hipFree(d_ring_);
+    (void)hipFree(d_buf_[0]);
+    (void)hipFree(d_buf_[1]);
+    (void)hipFree(d_ctl_);
+    (void)hipHostFree(h_ctl_);
+    if (own_stream_) (void)hipStreamDestroy(own_stream_);
+  }
+
+  size_t node_bytes() const override { return sizeof(Node); }
+  uintptr_t stream() const override { return reinterpret_cast<uintptr_t>(stream_); }
+  int device() const override { return cfg_.device; }
+  int grid() const { return grid_; }
+  // Device allocations (instance tables) released with the engine.
+  void adopt(void* device_ptr) { owned_.push_back(device_ptr); }
+
+  void push_host(const void* nodes, size_t n) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    if (n == 0) return;
+    sync_ctl();
+    normalize();
+    const Node* src = static_cast<const Node*>(nodes);
+    // keep at least half the ring free for in-flight growth; the rest waits on the host
+    const size_t room = cap_ / 2 > dev_stack() ? cap_ / 2 - dev_stack() : 0;
+    const size_t to_dev = std::min(n, room);
+    if (to_dev < n) spill_.insert(spill_.end(), src + to_dev, src + n);
+    ring_write_top(src, to_dev, hipMemcpyHostToDevice);
+    upload_ctl();
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  size_t pop_host(void* out, size_t max_n) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    normalize();
+    Node* dst = static_cast<Node*>(out);
+    size_t got = 0;
+    const size_t from_spill = std::min(max_n, spill_.size());
+    if (from_spill) {
+      std::copy(spill_.end() - from_spill, spill_.end(), dst);
+      spill_.resize(spill_.size() - from_spill);
+      got += from_spill;
+    }
+    const size_t from_dev = std::min(max_n - got, dev_stack());
+    ring_read_bottom(dst + got, from_dev, hipMemcpyDeviceToHost);
+    got += from_dev;
+    upload_ctl();
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    return got;
+  }
+
+  size_t export_device(void* dst, size_t max_n) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    normalize();
+    refill(max_n);
+    const size_t n = std::min(max_n, dev_stack());
+    ring_read_bottom(static_cast<Node*>(dst), n, hipMemcpyDeviceToDevice);
+    upload_ctl();
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    return n;
+  }
+
+  void import_device(const void* src, size_t n) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    if (n == 0) return;
+    sync_ctl();
+    normalize();
+    if (dev_stack() + n > cap_ / 2) {
+      // make room on the device: spill the ring bottom first
+      spill_bottom(dev_stack() + n - cap_ / 2);
+    }
+    ring_write_top(static_cast<const Node*>(src), n, hipMemcpyDeviceToDevice);
+    upload_ctl();
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  size_t size() override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    return dev_total() + spill_.size();
+  }
+
+  long run(long max_launches, double max_seconds, size_t stop_below) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    const auto t0 = std::chrono::steady_clock::now();
+    long launches = 0;
+    sync_ctl();
+    for (;;) {
+      if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
+      size_t total = dev_total();
+      if (total + spill_.size() == 0) break;
+      if (total + spill_.size() < stop_below) break;
+      if (max_launches >= 0 && launches >= max_launches) break;
+      if (max_seconds > 0 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >= max_seconds)
+        break;
+      // refill from the host spill when the device runs low
+      if (total < cfg_.max_parents && !spill_.empty()) {
+        normalize();
+        refill(cfg_.max_parents * 4);
+        upload_ctl();
+        total = dev_total();
+      }
+      // K iterations can grow the ring by at most K * buf_nodes_: keep headroom.
+      const bool ramp = total < cfg_.max_parents;
+      int gi = -1;
+      for (int i = static_cast<int>(ks_.size()) - 1; i >= 0; --i) {
+        if (ramp && i > 0) continue;
+        if (dev_total() + static_cast<size_t>(ks_[i] + 1) * buf_nodes_ <= cap_) {
+          gi = i;
+          break;
+        }
+      }
+      if (gi < 0) {
+        normalize();
+        spill_bottom(dev_stack() / 2 + 1);
+        upload_ctl();
+        continue;
+      }
+      launch_iters(gi);
+      ++launches;
+      sync_ctl();
+    }
+    stats_.t_run += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return launches;
+  }
+
+  void set_best(int b) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    h_ctl_->best.v = b;
+    upload_ctl();
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  int best() override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    return h_ctl_->best.v;
+  }
+  void reset_counters() override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    h_ctl_->tree.v = h_ctl_->sol.v = 0;
+    h_ctl_->parents = h_ctl_->iters = 0;
+    upload_ctl();
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  EngineStats stats() override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    EngineStats s = stats_;
+    s.tree = h_ctl_->tree.v;
+    s.sol = h_ctl_->sol.v;
+    s.parents = h_ctl_->parents;
+    s.iters = h_ctl_->iters;
+    s.best = h_ctl_->best.v;
+    s.device_nodes = dev_total();
+    s.host_nodes = spill_.size();
+    s.capacity = cap_;
+    return s;
+  }
+  void synchronize() override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+ private:
+  size_t dev_stack() const { return static_cast<size_t>(h_ctl_->stack[0].v); }
+  size_t dev_buf() const { return static_cast<size_t>(h_ctl_->buf[0].v); }
+  size_t dev_total() const { return dev_stack() + dev_buf(); }
+
+  void sync_ctl() {
+    const auto t0 = std::chrono::steady_clock::now();
+    TTS_HIP_CHECK(hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(dev::PoolCtl), hipMemcpyDeviceToHost, stream_));
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    ++stats_.syncs;
+    stats_.t_memcpy += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  void upload_ctl() {
+    TTS_HIP_CHECK(hipMemcpyAsync(d_ctl_, h_ctl_, sizeof(dev::PoolCtl), hipMemcpyHostToDevice, stream_));
+    // pinned source: make sure the copy consumed it before the host edits it again
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+
+  // Host shadow must be current (sync_ctl) and state slot 0 / buffer 0 active,
+  // which holds between graph replays (K is a multiple of 6).
+  void normalize() {
+    const size_t c = dev_buf();
+    if (c == 0) return;
+    ring_write_top(d_buf_[0], c, hipMemcpyDeviceToDevice);
+    h_ctl_->buf[0].v = 0;
+  }
+
+  void ring_write_top(const Node* src, size_t n, hipMemcpyKind kind) {
+    if (n == 0) return;
+    if (dev_stack() + n > cap_) throw std::runtime_error("device ring capacity exceeded");
+    const size_t start = (h_ctl_->bot + dev_stack()) & (cap_ - 1);
+    const size_t first = std::min(n, cap_ - start);
+    TTS_HIP_CHECK(hipMemcpyAsync(d_ring_ + start, src, first * sizeof(Node), kind, stream_));
+    if (first < n) TTS_HIP_CHECK(hipMemcpyAsync(d_ring_, src + first, (n - first) * sizeof(Node), kind, stream_));
+    h_ctl_->stack[0].v += n;
+  }
+
+  void ring_read_bottom(Node* dst, size_t n, hipMemcpyKind kind) {
+    if (n == 0) return;
+    const size_t start = h_ctl_->bot & (cap_ - 1);
+    const size_t first = std::min(n, cap_ - start);
+    TTS_HIP_CHECK(hipMemcpyAsync(dst, d_ring_ + start, first * sizeof(Node), kind, stream_));
+    if (first < n) TTS_HIP_CHECK(hipMemcpyAsync(dst + first, d_ring_, (n - first) * sizeof(Node), kind, stream_));
+    if (kind != hipMemcpyDeviceToDevice) TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    h_ctl_->bot = (h_ctl_->bot + n) & (cap_ - 1);
+    h_ctl_->stack[0].v -= n;
+  }
+
+  void spill_bottom(size_t n) {
+    n = std::min(n, dev_stack());
+    if (n == 0) return;
+    const size_t old = spill_.size();
+    spill_.resize(old + n);
+    // oldest device nodes go to the end of the host spill (taken first on refill)
+    std::vector<Node> tmp(n);
+    ring_read_bottom(tmp.data(), n, hipMemcpyDeviceToHost);
+    std::copy(tmp.begin(), tmp.end(), spill_.begin() + old);
+    stats_.spilled += n;
+  }
+
+  void refill(size_t want) {
+    const size_t n = std::min(want, spill_.size());
+    if (n == 0) return;
+    const size_t room = cap_ / 2 > dev_stack() ? cap_ / 2 - dev_stack() : 0;
+    const size_t m = std::min(n, room);
+    if (m == 0) return;
+    ring_write_top(spill_.data() + (spill_.size() - m), m, hipMemcpyHostToDevice);
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    spill_.resize(spill_.size() - m);
+    stats_.refilled += m;
+  }
+
+  void launch_iters(int gi) {
+    if (cfg_.use_graphs) {
+      TTS_HIP_CHECK(hipGraphLaunch(graphs_[gi], stream_));
+    } else {
+      for (int i = 0; i < ks_[gi]; ++i) Traits::launch(args_, i % 6, grid_, stream_);
+      TTS_HIP_CHECK(hipGetLastError());
+    }
+    ++stats_.launches;
+  }
+
+  hipGraphExec_t capture(int K) {
+    hipStream_t cs;
+    TTS_HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraph_t g;
+    TTS_HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < K; ++i) Traits::launch(args_, i % 6, grid_, cs);
+    TTS_HIP_CHECK(hipStreamEndCapture(cs, &g));
+    hipGraphExec_t exec;
+    TTS_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    TTS_HIP_CHECK(hipGraphDestroy(g));
+    TTS_HIP_CHECK(hipStreamDestroy(cs));
+    return exec;
+  }
+
+  EngineConfig cfg_;
+  Args args_;
+  size_t cap_ = 0, buf_nodes_ = 0, max_children_ = 0;
+  int grid_ = 1;
+  Node* d_ring_ = nullptr;
+  Node* d_buf_[2] = {nullptr, nullptr};
+  dev::PoolCtl* d_ctl_ = nullptr;
+  dev::PoolCtl* h_ctl_ = nullptr;
+  hipStream_t stream_ = nullptr, own_stream_ = nullptr;
+  std::vector<int> ks_;
+  std::vector<hipGraphExec_t> graphs_;
+  std::vector<void*> owned_;
+  std::vector<Node> spill_;
+  EngineStats stats_;
+};
+
+}  // namespace tts

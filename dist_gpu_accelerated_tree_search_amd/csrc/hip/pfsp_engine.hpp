@@ -1,0 +1,182 @@
+// PFSP device engine: instance tables on the GPU + engine traits + factories.
+//
+// Parity: ref lb1_alloc_gpu / lb2_alloc_gpu (PFSP_gpu_lib.cu:154-200) deep-copy the
+// bound tables once per GPU thread (and leak them). Here the tables
+// are built once in the layout the kernels stage into LDS:
+//   ptab  job-major u16 rows padded to 16 B        (LB1 / LB1_d / LB2 fronts)
+//   recs  per machine pair, the Johnson order as {job, p0, p1, lag} u16 records,
+//         so one wave-uniform 8-B read drives one Johnson step for 64 children.
+// and are owned (freed) by the engine.
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "../core/pfsp_instance.hpp"
+#include "engine.hpp"
+#include "pfsp_kernels.hpp"
+
+namespace tts {
+
+template <int NJ, int M, int LBK>
+struct PfspTraits {
+  using Node = PfspNode<NJ>;
+  using Args = dev::PfspArgs<NJ, M>;
+  static void launch(const Args& a, int t, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
+  }
+  static int blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_expand_kernel<NJ, M, LBK>, dev::kBlock, 0) !=
+        hipSuccess)
+      return 1;
+    return n;
+  }
+  static int parents_per_block() { return dev::PfspGeom<NJ>::BP; }
+};
+
+// Host-side images of the device tables.
+struct PfspTableImages {
+  std::vector<uint16_t> ptab;  // [N][MS]
+  std::vector<uint2> recs;     // [P][N]
+};
+
+template <int NJ, int M>
+inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, M>& a) {
+  using C = dev::PfspConsts<M>;
+  if (in.machines != M) throw std::invalid_argument("machine count does not match kernel instantiation");
+  if (in.jobs > NJ) throw std::invalid_argument("job count exceeds kernel bucket");
+  PfspTableImages img;
+  img.ptab.assign(static_cast<size_t>(in.jobs) * C::MS, 0);
+  for (int j = 0; j < in.jobs; ++j)
+    for (int m = 0; m < M; ++m) img.ptab[static_cast<size_t>(j) * C::MS + m] = static_cast<uint16_t>(in.pt(m, j));
+  img.recs.resize(static_cast<size_t>(C::P) * in.jobs);
+  for (int q = 0; q < C::P; ++q) {
+    const int m0 = in.pair_m0[q], m1 = in.pair_m1[q];
+    for (int r = 0; r < in.jobs; ++r) {
+      const int job = in.johnson[static_cast<size_t>(q) * in.jobs + r];
+      const int lag = in.lags[static_cast<size_t>(q) * in.jobs + job];
+      if (lag > 0xffff) throw std::invalid_argument("LB2 lag does not fit 16 bits");
+      uint2 rc;
+      rc.x = static_cast<uint32_t>(job) | (static_cast<uint32_t>(in.pt(m0, job)) << 16);
+      rc.y = static_cast<uint32_t>(in.pt(m1, job)) | (static_cast<uint32_t>(lag) << 16);
+      img.recs[static_cast<size_t>(q) * in.jobs + r] = rc;
+    }
+  }
+  a.jobs = in.jobs;
+  for (int m = 0; m < M; ++m) {
+    a.min_heads[m] = in.min_heads[m];
+    a.min_tails[m] = in.min_tails[m];
+    long s = 0;
+    for (int j = 0; j < in.jobs; ++j) s += in.pt(m, j);
+    // front and remain are packed as two u16 per machine in LDS
+    if (s > 0xffff) throw std::invalid_argument("instance too large for 16-bit schedule packing");
+    a.sum_all[m] = static_cast<int>(s);
+  }
+  for (int q = 0; q < C::P; ++q) {
+    a.pm0[q] = static_cast<uint8_t>(in.pair_m0[q]);
+    a.pm1[q] = static_cast<uint8_t>(in.pair_m1[q]);
+  }
+  return img;
+}
+
+template <class T>
+inline T* upload_vec(const std::vector<T>& v) {
+  T* d = nullptr;
+  TTS_HIP_CHECK(hipMalloc(&d, std::max<size_t>(1, v.size()) * sizeof(T)));
+  if (!v.empty()) TTS_HIP_CHECK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+template <int NJ, int M, int LBK>
+std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const EngineConfig& cfg) {
+  TTS_HIP_CHECK(hipSetDevice(cfg.device));
+  dev::PfspArgs<NJ, M> a{};
+  const PfspTableImages img = pfsp_fill_args(in, a);
+  a.ptab = upload_vec(img.ptab);
+  a.recs = upload_vec(img.recs);
+  auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a, NJ);
+  eng->adopt(const_cast<uint16_t*>(a.ptab));
+  eng->adopt(const_cast<uint2*>(a.recs));
+  return eng;
+}
+
+// Reference-style batch evaluation on the GPU (host arrays in and out):
+// bounds of every child of every parent, in parent order, children k = depth..N-1.
+template <int NJ, int M, int LBK>
+std::vector<int> pfsp_gpu_bounds_t(const PfspInstance& in, const void* parents, size_t n, int best, int device) {
+  using Node = PfspNode<NJ>;
+  TTS_HIP_CHECK(hipSetDevice(device));
+  dev::PfspArgs<NJ, M> a{};
+  const PfspTableImages img = pfsp_fill_args(in, a);
+  const Node* ph = static_cast<const Node*>(parents);
+  std::vector<int> offsets(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + (in.jobs - ph[i].depth);
+  const size_t nb = static_cast<size_t>(offsets[n]);
+  std::vector<int> out(nb, 0);
+  if (n == 0) return out;
+  a.ptab = upload_vec(img.ptab);
+  a.recs = upload_vec(img.recs);
+  a.offsets = upload_vec(offsets);
+  Node* dparents = nullptr;
+  int* dbounds = nullptr;
+  TTS_HIP_CHECK(hipMalloc(&dparents, n * sizeof(Node)));
+  TTS_HIP_CHECK(hipMalloc(&dbounds, std::max<size_t>(1, nb) * sizeof(int)));
+  TTS_HIP_CHECK(hipMemcpy(dparents, ph, n * sizeof(Node), hipMemcpyHostToDevice));
+  a.parents_in = dparents;
+  a.bounds_out = dbounds;
+  a.nparents = static_cast<int>(n);
+  a.best_in = best;
+  const int nchunks = static_cast<int>((n + dev::PfspGeom<NJ>::BP - 1) / dev::PfspGeom<NJ>::BP);
+  hipLaunchKernelGGL((dev::pfsp_bounds_kernel<NJ, M, LBK>), dim3(std::min(nchunks, 2048)), dim3(dev::kBlock), 0, 0, a);
+  TTS_HIP_CHECK(hipGetLastError());
+  TTS_HIP_CHECK(hipDeviceSynchronize());
+  TTS_HIP_CHECK(hipMemcpy(out.data(), dbounds, nb * sizeof(int), hipMemcpyDeviceToHost));
+  (void)hipFree(dparents);
+  (void)hipFree(dbounds);
+  (void)hipFree(const_cast<int*>(a.offsets));
+  (void)hipFree(const_cast<uint16_t*>(a.ptab));
+  (void)hipFree(const_cast<uint2*>(a.recs));
+  return out;
+}
+
+// ---- run-time dispatch (definitions in pfsp_engine_nj*.hip, one TU per bucket) ----
+std::unique_ptr<IEngine> make_pfsp_engine(const PfspInstance& in, int lb, const EngineConfig& cfg);
+std::vector<int> pfsp_gpu_bounds(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device);
+
+#define TTS_PFSP_DECLARE_BUCKET(NJ)                                                                   \
+  std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg); \
+  std::vector<int> pfsp_gpu_bounds_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
+                                          int device);
+TTS_PFSP_DECLARE_BUCKET(20)
+TTS_PFSP_DECLARE_BUCKET(50)
+TTS_PFSP_DECLARE_BUCKET(100)
+TTS_PFSP_DECLARE_BUCKET(200)
+TTS_PFSP_DECLARE_BUCKET(500)
+
+// Body of one bucket's TU: machines 5 / 10 / 20, LB kernels 1 (LB1 and LB1_d) / 2.
+#define TTS_PFSP_DEFINE_BUCKET(NJ)                                                                     \
+  std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg) { \
+    const bool l2 = (lb == 2);                                                                         \
+    switch (in.machines) {                                                                             \
+      case 5: return l2 ? make_pfsp_engine_t<NJ, 5, 2>(in, cfg) : make_pfsp_engine_t<NJ, 5, 1>(in, cfg);     \
+      case 10: return l2 ? make_pfsp_engine_t<NJ, 10, 2>(in, cfg) : make_pfsp_engine_t<NJ, 10, 1>(in, cfg);  \
+      case 20: return l2 ? make_pfsp_engine_t<NJ, 20, 2>(in, cfg) : make_pfsp_engine_t<NJ, 20, 1>(in, cfg);  \
+      default: throw std::invalid_argument("GPU kernels are instantiated for 5, 10 or 20 machines");        \
+    }                                                                                                  \
+  }                                                                                                    \
+  std::vector<int> pfsp_gpu_bounds_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
+                                          int device) {                                                \
+    const bool l2 = (lb == 2);                                                                         \
+    switch (in.machines) {                                                                             \
+      case 5: return l2 ? pfsp_gpu_bounds_t<NJ, 5, 2>(in, parents, n, best, device)                    \
+                        : pfsp_gpu_bounds_t<NJ, 5, 1>(in, parents, n, best, device);                   \
+      case 10: return l2 ? pfsp_gpu_bounds_t<NJ, 10, 2>(in, parents, n, best, device)                  \
+                         : pfsp_gpu_bounds_t<NJ, 10, 1>(in, parents, n, best, device);                 \
+      case 20: return l2 ? pfsp_gpu_bounds_t<NJ, 20, 2>(in, parents, n, best, device)                  \
+                         : pfsp_gpu_bounds_t<NJ, 20, 1>(in, parents, n, best, device);                 \
+      default: throw std::invalid_argument("GPU kernels are instantiated for 5, 10 or 20 machines");        \
+    }                                                                                                  \
+  }
+
+}  // namespace tts

@@ -1,0 +1,415 @@
+// PFSP search kernels for gfx950 (CDNA4).
+//
+// What the reference does (ref pfsp/lib/PFSP_gpu_lib.cu:43-152, bounds_gpu.cu):
+// one thread per child (LB1/LB2) or per parent (LB1_d), each copying the 44-B node
+// and 20-int arrays into scratch (176-256 B/lane spilled on gfx950), no LDS, a
+// synchronous bounds round trip to the host, and child generation on the CPU.
+//
+// What happens here, per 256-thread workgroup and per chunk of BP parents:
+//   Phase A  thread-per-parent: parent nodes -> LDS; the parent's schedule prefix is
+//            replayed once (front[M] = completion times, remain[M] = unscheduled
+//            work) from the LDS-staged job-major p table; both packed u16|u16 into
+//            one LDS row per parent. Child counts are scanned across the workgroup
+//            and a child->parent map is written to LDS.
+//   Phase B  thread-per-child: LB1 (== LB1_d) costs O(M) per child from
+//            the parent's LDS row. LB2 walks each machine pair's Johnson order with
+//            wave-uniform records (one LDS broadcast per step) and a per-lane
+//            scheduled-set bitmask, exiting a lane as soon as lb > best (ref
+//            c_bound_johnson.c:211-237, same pair order => same prune decisions).
+//   Phase C  (expand kernel) prune + stream compaction: one 64-bit ballot per wave
+//            into an LDS bitmap, a popcount scan, ONE device atomic per chunk to
+//            reserve output slots, then each survivor writes its child node
+//            straight into the device-resident pool. Leaves update sol and the
+//            incumbent (atomicMin), exactly the counting rules of
+//            ref PFSP_lib.h:51-95 (generate_children).
+// Nothing returns to the host per iteration.
+#pragma once
+
+#include <climits>
+
+#include "../core/pfsp_node.hpp"
+#include "device_common.hpp"
+
+namespace tts {
+namespace dev {
+
+template <int NJ>
+struct PfspGeom {
+  static constexpr int BP = NJ <= 50 ? 256 : (NJ <= 100 ? 128 : (NJ <= 200 ? 64 : 32));  // parents per chunk
+  static constexpr int MAXCH = BP * NJ;                  // children per chunk (upper bound)
+  static constexpr int NWORDS = (MAXCH + 63) / 64;       // survivor bitmap words
+  static constexpr int NW = (NJ + 63) / 64;              // 64-bit words of a job set
+  using map_t = std::conditional_t<(BP <= 256), uint8_t, uint16_t>;
+  static_assert(NWORDS <= kBlock, "survivor bitmap scan assumes <= 256 words");
+};
+
+template <int M>
+struct PfspConsts {
+  static constexpr int P = M * (M - 1) / 2;
+  static constexpr int MS = (M + 7) & ~7;  // u16 row stride of the LDS p table (16-B rows)
+};
+
+// Kernel arguments (by value -> kernarg segment -> SGPRs for the uniform tables).
+template <int NJ, int M>
+struct PfspArgs {
+  PfspNode<NJ>* stack;     // ring buffer, cap_mask+1 nodes
+  PfspNode<NJ>* buf[2];    // children buffers (ping-pong), max_parents*NJ nodes each
+  PoolCtl* ctl;
+  const uint16_t* ptab;    // job-major p, [jobs][MS]
+  const uint2* recs;       // LB2 Johnson records, [P][jobs]: {job | p0<<16, p1 | lag<<16}
+  const int* offsets;      // bounds kernel only: exclusive prefix of child counts
+  int* bounds_out;         // bounds kernel only
+  const PfspNode<NJ>* parents_in;  // bounds kernel only
+  u64 cap_mask;
+  int jobs;
+  int max_parents;
+  int nparents;            // bounds kernel only
+  int best_in;             // bounds kernel only
+  int min_heads[M];
+  int min_tails[M];
+  int sum_all[M];
+  uint8_t pm0[PfspConsts<M>::P];
+  uint8_t pm1[PfspConsts<M>::P];
+};
+
+template <int NJ, int M, int LBK>
+struct PfspSmem {
+  using G = PfspGeom<NJ>;
+  using C = PfspConsts<M>;
+  static constexpr bool kRecsInLds = (LBK == 2) && (C::P * NJ * 8 <= 32 * 1024);
+  PfspNode<NJ> node[G::BP];
+  uint32_t fr[G::BP][M];                          // front | remain << 16
+  uint16_t ptab[NJ][C::MS];
+  int off[G::BP];
+  typename G::map_t map[G::MAXCH];
+  u64 bits[G::NWORDS + kBlock / kWave];
+  int wpre[kBlock];
+  int scan[kBlock / kWave];
+  u64 base;
+  u64 pmask[LBK == 2 ? G::BP : 1][G::NW];         // scheduled set (LB2)
+  uint16_t cf[LBK == 2 ? kBlock : 1][M];          // child front (LB2)
+  uint2 recs[kRecsInLds ? C::P * NJ : 1];
+};
+
+// ---------------------------------------------------------------------------
+// Phase A: stage `nvalid` parents (fetched through `src(i)`) and their prefixes.
+// Returns the number of children of the chunk.
+template <int NJ, int M, int LBK, class Src>
+__device__ inline int pfsp_phase_a(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm, int nvalid, Src src) {
+  using G = PfspGeom<NJ>;
+  using Node = PfspNode<NJ>;
+  constexpr int VPN = sizeof(Node) / 16;
+  const int tid = threadIdx.x;
+  // coalesced node copy: VPN 16-byte vectors per node
+  for (int v = tid; v < nvalid * VPN; v += kBlock) {
+    const int i = v / VPN, w = v - i * VPN;
+    reinterpret_cast<uint4*>(&sm.node[i])[w] = reinterpret_cast<const uint4*>(src(i))[w];
+  }
+  __syncthreads();
+  int nchild = 0;
+  if (tid < nvalid) {
+    const Node& nd = sm.node[tid];
+    const int d = nd.depth;
+    int f[M], r[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      f[m] = (d == 0) ? a.min_heads[m] : 0;
+      r[m] = a.sum_all[m];
+    }
+    u64 msk[G::NW];
+#pragma unroll
+    for (int w = 0; w < G::NW; ++w) msk[w] = 0;
+    for (int i = 0; i < d; ++i) {
+      const int job = nd.prmu[i];
+      const uint16_t* row = sm.ptab[job];
+      int pr[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) pr[m] = row[m];
+      f[0] += pr[0];
+      r[0] -= pr[0];
+#pragma unroll
+      for (int m = 1; m < M; ++m) {
+        f[m] = max(f[m - 1], f[m]) + pr[m];
+        r[m] -= pr[m];
+      }
+      if constexpr (LBK == 2) {
+#pragma unroll
+        for (int w = 0; w < G::NW; ++w)
+          if ((job >> 6) == w) msk[w] |= 1ull << (job & 63);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) sm.fr[tid][m] = static_cast<uint32_t>(f[m]) | (static_cast<uint32_t>(r[m]) << 16);
+    if constexpr (LBK == 2) {
+#pragma unroll
+      for (int w = 0; w < G::NW; ++w) sm.pmask[tid][w] = msk[w];
+    }
+    nchild = a.jobs - d;
+  }
+  int total = 0;
+  const int off = block_exclusive_scan(nchild, sm.scan, &total);
+  if (tid < nvalid) {
+    sm.off[tid] = off;
+    for (int j = 0; j < nchild; ++j) sm.map[off + j] = static_cast<typename G::map_t>(tid);
+  }
+  __syncthreads();
+  return total;
+}
+
+template <int NW>
+__device__ inline bool job_in(const u64 (&msk)[NW], int job) {
+  if constexpr (NW == 1) {
+    return (msk[0] >> job) & 1ull;
+  } else {
+    u64 word = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) word = ((job >> 6) == w) ? msk[w] : word;
+    return (word >> (job & 63)) & 1ull;
+  }
+}
+
+// Where phase B reads the LB2 records from: LDS when they fit (staged once per
+// workgroup), otherwise global memory (uniform addresses -> broadcast / L2 hits).
+template <int NJ, int M, int LBK>
+struct SmemRecs {
+  __device__ static const uint2* get(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm) {
+    if constexpr (PfspSmem<NJ, M, LBK>::kRecsInLds)
+      return sm.recs;
+    else
+      return a.recs;
+  }
+};
+
+// Phase B: bound of child c of the staged chunk. Sets p (chunk parent), k (prmu
+// position moved to the front), job.
+template <int NJ, int M, int LBK>
+__device__ inline int pfsp_child_bound(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm, int c, int best, int& p,
+                                       int& k, int& job) {
+  using G = PfspGeom<NJ>;
+  using C = PfspConsts<M>;
+  p = sm.map[c];
+  const int d = sm.node[p].depth;
+  k = d + (c - sm.off[p]);
+  job = sm.node[p].prmu[k];
+  const uint16_t* row = sm.ptab[job];
+  const uint32_t* fr = sm.fr[p];
+  if constexpr (LBK != 2) {
+    // LB1 / LB1_d: max over machines of child front + child remain + min tail.
+    const int f0 = fr[0] & 0xffff, r0 = fr[0] >> 16;
+    int lb = f0 + r0 + a.min_tails[0];
+    int t = f0 + row[0];
+#pragma unroll
+    for (int m = 1; m < M; ++m) {
+      const int fm = fr[m] & 0xffff, rm = fr[m] >> 16;
+      const int s = max(t, fm);
+      lb = max(lb, s + rm + a.min_tails[m]);
+      t = s + row[m];
+    }
+    return lb;
+  } else {
+    // LB2: child front, then the Johnson walk of every machine pair.
+    uint16_t* cf = sm.cf[threadIdx.x];
+    {
+      int t = (fr[0] & 0xffff) + row[0];
+      cf[0] = static_cast<uint16_t>(t);
+#pragma unroll
+      for (int m = 1; m < M; ++m) {
+        t = max(t, static_cast<int>(fr[m] & 0xffff)) + row[m];
+        cf[m] = static_cast<uint16_t>(t);
+      }
+    }
+    u64 msk[G::NW];
+#pragma unroll
+    for (int w = 0; w < G::NW; ++w) msk[w] = sm.pmask[p][w] | (((job >> 6) == w) ? (1ull << (job & 63)) : 0ull);
+    const uint2* recs = SmemRecs<NJ, M, LBK>::get(a, sm);
+    const int N = a.jobs;
+    int lb = 0;
+    for (int q = 0; q < C::P; ++q) {
+      const int ma0 = a.pm0[q], ma1 = a.pm1[q];
+      int t0 = cf[ma0], t1 = cf[ma1];
+      const uint2* rq = recs + q * N;
+#pragma unroll 4
+      for (int r = 0; r < N; ++r) {
+        const uint2 rc = rq[r];
+        const int jb = rc.x & 0xffff;
+        const int p0 = rc.x >> 16, p1 = rc.y & 0xffff, lag = rc.y >> 16;
+        const int n0 = t0 + p0;
+        const int n1 = max(t1, n0 + lag) + p1;
+        const bool sched = job_in<G::NW>(msk, jb);
+        t0 = sched ? t0 : n0;
+        t1 = sched ? t1 : n1;
+      }
+      lb = max(lb, max(t1 + a.min_tails[ma1], t0 + a.min_tails[ma0]));
+      if (lb > best) break;
+    }
+    return lb;
+  }
+}
+
+template <int NJ, int M, int LBK>
+__device__ inline void pfsp_stage_tables(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm) {
+  using C = PfspConsts<M>;
+  const int tid = threadIdx.x;
+  const int nrow = a.jobs * C::MS;
+  uint16_t* pt = &sm.ptab[0][0];
+  for (int i = tid; i < nrow; i += kBlock) pt[i] = a.ptab[i];
+  if constexpr (PfspSmem<NJ, M, LBK>::kRecsInLds) {
+    const int nrec = C::P * a.jobs;
+    for (int i = tid; i < nrec; i += kBlock) sm.recs[i] = a.recs[i];
+  }
+  __syncthreads();
+}
+
+// Write one id (element e = 1 + position, element 0 = depth) into a node held as
+// 32-bit words in registers; every word is touched with a select so the node
+// never spills to scratch.
+template <int NJ, int NWD>
+__device__ inline void node_set(uint32_t (&w)[NWD], int e, uint32_t v) {
+  using id_t = typename PfspNode<NJ>::id_t;
+  constexpr int per = 4 / sizeof(id_t);
+  constexpr uint32_t mask = sizeof(id_t) == 1 ? 0xffu : 0xffffu;
+  const int wi = e / per;
+  const int sh = (e % per) * 8 * sizeof(id_t);
+#pragma unroll
+  for (int i = 0; i < NWD; ++i) w[i] = (i == wi) ? ((w[i] & ~(mask << sh)) | (v << sh)) : w[i];
+}
+
+// ---------------------------------------------------------------------------
+// One B&B iteration on the device-resident pool (see PoolCtl). `t` in [0, 6):
+// state record t%3, children buffer parity t%2.
+template <int NJ, int M, int LBK>
+__global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
+  using G = PfspGeom<NJ>;
+  using Node = PfspNode<NJ>;
+  constexpr int VPN = sizeof(Node) / 16;
+  constexpr int NWD = sizeof(Node) / 4;
+  __shared__ PfspSmem<NJ, M, LBK> sm;
+  const int tid = threadIdx.x;
+  const int s_in = t % 3, s_out = (t + 1) % 3, s_zero = (t + 2) % 3;
+  Node* const bin = a.buf[t & 1];
+  Node* const bout = a.buf[(t & 1) ^ 1];
+  PoolCtl* ctl = a.ctl;
+
+  const u64 S = ctl->stack[s_in].v;
+  const u64 Cn = ctl->buf[s_in].v;
+  const u64 bot = ctl->bot;
+  const u64 B = min(S + Cn, static_cast<u64>(a.max_parents));
+  const u64 nb = min(B, Cn);
+  const u64 ns = B - nb;
+  const u64 L = Cn - nb;  // children of the last iteration not expanded now
+  const u64 Snew = S - ns + L;
+  const bool overflow = Snew > a.cap_mask + 1;
+  const int best = __hip_atomic_load(&ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+  if (blockIdx.x == 0 && tid == 0) {
+    ctl->stack[s_out].v = overflow ? S : Snew;
+    ctl->stack[s_zero].v = 0;
+    ctl->buf[s_zero].v = 0;
+    if (B > 0) {
+      ctl->parents += B;
+      ctl->iters += 1;
+    }
+    if (overflow) ctl->overflow = 1;
+  }
+  if (B == 0 || overflow) return;
+
+  // Leftover children -> top of the ring (disjoint from the parents read below).
+  for (u64 v = static_cast<u64>(blockIdx.x) * kBlock + tid; v < L * VPN; v += static_cast<u64>(gridDim.x) * kBlock) {
+    const u64 i = v / VPN, w = v - i * VPN;
+    const u64 slot = (bot + S + i) & a.cap_mask;
+    reinterpret_cast<uint4*>(a.stack + slot)[w] = reinterpret_cast<const uint4*>(bin + i)[w];
+  }
+
+  pfsp_stage_tables(a, sm);
+  const u64 nchunks = (B + G::BP - 1) / G::BP;
+  u64 my_sol = 0;
+  for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const u64 first = ch * G::BP;
+    const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), B - first));
+    const int total = pfsp_phase_a(a, sm, nvalid, [&](int i) -> const Node* {
+      const u64 gi = first + i;
+      if (gi < nb) return bin + (Cn - nb + gi);
+      return a.stack + ((bot + S - ns + (gi - nb)) & a.cap_mask);
+    });
+    // Phase B: bounds, leaves, survivor bitmap.
+    for (int cb = 0; cb < total; cb += kBlock) {
+      const int c = cb + tid;
+      bool survive = false;
+      if (c < total) {
+        int p, k, job;
+        const int lb = pfsp_child_bound(a, sm, c, best, p, k, job);
+        const bool leaf = sm.node[p].depth + 1 == a.jobs;
+        if (leaf) {
+          ++my_sol;
+          if (lb < best) atomicMin(&ctl->best.v, lb);
+        } else {
+          survive = lb < best;
+        }
+      }
+      const u64 bal = __ballot(survive);
+      if ((tid & (kWave - 1)) == 0) sm.bits[c >> 6] = bal;
+    }
+    __syncthreads();
+    // Phase C: compaction + one atomic slot reservation per chunk.
+    const int nwords = (total + 63) >> 6;
+    int nsurv = 0;
+    const int wp = block_exclusive_scan(tid < nwords ? __popcll(sm.bits[tid]) : 0, sm.scan, &nsurv);
+    sm.wpre[tid] = wp;
+    if (tid == 0) {
+      sm.base = nsurv ? atomicAdd(&ctl->buf[s_out].v, static_cast<u64>(nsurv)) : 0;
+      if (nsurv) atomicAdd(&ctl->tree.v, static_cast<u64>(nsurv));
+    }
+    __syncthreads();
+    const u64 base = sm.base;
+    for (int c = tid; c < total; c += kBlock) {
+      const u64 word = sm.bits[c >> 6];
+      if (!((word >> (c & 63)) & 1ull)) continue;
+      const int rank = sm.wpre[c >> 6] + __popcll(word & ((1ull << (c & 63)) - 1ull));
+      const int p = sm.map[c];
+      const int d = sm.node[p].depth;
+      const int k = d + (c - sm.off[p]);
+      uint32_t w[NWD];
+#pragma unroll
+      for (int i = 0; i < NWD; ++i) w[i] = reinterpret_cast<const uint32_t*>(&sm.node[p])[i];
+      const uint32_t jd = sm.node[p].prmu[d], jk = sm.node[p].prmu[k];
+      node_set<NJ>(w, 0, static_cast<uint32_t>(d + 1));
+      node_set<NJ>(w, 1 + d, jk);
+      node_set<NJ>(w, 1 + k, jd);
+      uint4* dst = reinterpret_cast<uint4*>(bout + base + rank);
+#pragma unroll
+      for (int v = 0; v < VPN; ++v) dst[v] = make_uint4(w[4 * v], w[4 * v + 1], w[4 * v + 2], w[4 * v + 3]);
+    }
+    __syncthreads();
+  }
+  // sol: wave reduction then one atomic per wave
+  u64 s = my_sol;
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+  if ((tid & (kWave - 1)) == 0 && s) atomicAdd(&ctl->sol.v, s);
+}
+
+// Reference-style evaluation (ref evaluate_gpu, PFSP_gpu_lib.cu:129-152): bounds of
+// every child of `nparents` parents, bounds_out[offsets[i] + (k - depth_i)].
+template <int NJ, int M, int LBK>
+__global__ __launch_bounds__(kBlock) void pfsp_bounds_kernel(PfspArgs<NJ, M> a) {
+  using G = PfspGeom<NJ>;
+  using Node = PfspNode<NJ>;
+  __shared__ PfspSmem<NJ, M, LBK> sm;
+  const int tid = threadIdx.x;
+  pfsp_stage_tables(a, sm);
+  const int nchunks = (a.nparents + G::BP - 1) / G::BP;
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int first = ch * G::BP;
+    const int nvalid = min(G::BP, a.nparents - first);
+    const int total = pfsp_phase_a(a, sm, nvalid, [&](int i) -> const Node* { return a.parents_in + first + i; });
+    for (int c = tid; c < total; c += kBlock) {
+      int p, k, job;
+      const int lb = pfsp_child_bound(a, sm, c, a.best_in, p, k, job);
+      a.bounds_out[a.offsets[first + p] + (k - sm.node[p].depth)] = lb;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace dev
+}  // namespace tts

@@ -1,0 +1,60 @@
+// N-Queens device engine (traits + factory) and reference-style label evaluation.
+#include "queens_engine.hpp"
+#include "queens_kernels.hpp"
+
+namespace tts {
+
+struct QueensTraits {
+  using Node = QueensNode;
+  using Args = dev::QueensArgs;
+  static void launch(const Args& a, int t, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(dev::queens_expand_kernel, dim3(grid), dim3(dev::kBlock), 0, s, a, t);
+  }
+  static int blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::queens_expand_kernel, dev::kBlock, 0) != hipSuccess)
+      return 1;
+    return n;
+  }
+  static int parents_per_block() { return dev::QueensSmem::BP; }
+};
+
+static dev::QueensArgs queens_args(int N, int G) {
+  if (N < 1 || N > 32) throw std::invalid_argument("N-Queens supports 1 <= N <= 32");
+  if (G < 1) throw std::invalid_argument("g must be >= 1");
+  dev::QueensArgs a{};
+  a.N = N;
+  a.G = G;
+  a.full = N == 32 ? 0xffffffffu : ((1u << N) - 1u);
+  return a;
+}
+
+std::unique_ptr<IEngine> make_queens_engine(int N, int G, const EngineConfig& cfg) {
+  TTS_HIP_CHECK(hipSetDevice(cfg.device));
+  return std::make_unique<DeviceEngine<QueensTraits>>(cfg, queens_args(N, G), N);
+}
+
+std::vector<uint8_t> queens_gpu_labels(int N, int G, const QueensNode* parents, size_t n, int device) {
+  TTS_HIP_CHECK(hipSetDevice(device));
+  dev::QueensArgs a = queens_args(N, G);
+  std::vector<uint8_t> out(n * static_cast<size_t>(N), 0);
+  if (n == 0) return out;
+  QueensNode* dp = nullptr;
+  uint8_t* dl = nullptr;
+  TTS_HIP_CHECK(hipMalloc(&dp, n * sizeof(QueensNode)));
+  TTS_HIP_CHECK(hipMalloc(&dl, out.size()));
+  TTS_HIP_CHECK(hipMemcpy(dp, parents, n * sizeof(QueensNode), hipMemcpyHostToDevice));
+  a.parents_in = dp;
+  a.labels_out = dl;
+  a.nparents = static_cast<int>(n);
+  const int blocks = static_cast<int>((n + dev::kBlock - 1) / dev::kBlock);
+  hipLaunchKernelGGL(dev::queens_labels_kernel, dim3(blocks), dim3(dev::kBlock), 0, 0, a);
+  TTS_HIP_CHECK(hipGetLastError());
+  TTS_HIP_CHECK(hipDeviceSynchronize());
+  TTS_HIP_CHECK(hipMemcpy(out.data(), dl, out.size(), hipMemcpyDeviceToHost));
+  (void)hipFree(dp);
+  (void)hipFree(dl);
+  return out;
+}
+
+}  // namespace tts
