@@ -1,0 +1,220 @@
+"""Command line (parity with the reference executables' flags, defaults and output).
+
+    python -m dist_gpu_accelerated_tree_search_amd pfsp  [-i 14 -l 1 -u 1 -m 25 -M 50000 -T 5000 -D 1 -C 0 -w 1 -L 1 -p 50]
+    python -m dist_gpu_accelerated_tree_search_amd nqueens [-N 14 -g 1 -m 25 -M 50000 -D 1]
+
+pfsp:  -D 0            CPU only: -C threads (0/1 = sequential, ref pfsp_c / pfsp_omp_c)
+       -D 1            one GPU (ref pfsp_multigpu_cuda.out -D 1)
+       -D N            N GPUs, one process per GPU (ranks spawned here, or run the
+                       same command under torchrun); -w / -L enable work sharing
+                       inside a node / across nodes (ref -w, -L); -C 1 adds CPU
+                       workers on each rank (ref -C).
+nqueens: -D 0 CPU sequential (ref nqueens_c), -D >= 1 GPU(s).
+Results: the reference's stdout blocks, plus a CSV row (singlegpu.csv,
+multigpu.csv or dist_multigpu.csv) and optionally a JSON record (--json).
+-M is the reference's per-offload batch cap; the device engine's per-iteration
+parent window is --max-parents (default 262144, sized for 288 GB HBM).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+from .utils import report
+
+INT_MAX = 2**31 - 1
+
+
+def _pfsp_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="pfsp", description="PFSP Branch-and-Bound (Taillard instances)")
+    ap.add_argument("-i", "--inst", type=int, default=14)
+    ap.add_argument("-l", "--lb", type=int, default=1)
+    ap.add_argument("-u", "--ub", type=int, default=1)
+    ap.add_argument("-m", "--m", type=int, default=25)
+    ap.add_argument("-M", "--M", type=int, default=50000)
+    ap.add_argument("-T", "--T", type=int, default=5000)
+    ap.add_argument("-D", "--D", type=int, default=1)
+    ap.add_argument("-C", "--C", type=int, default=0)
+    ap.add_argument("-w", "--ws", type=int, default=1)
+    ap.add_argument("-L", "--L", type=int, default=1)
+    ap.add_argument("-p", "--perc", type=int, default=50)
+    ap.add_argument("--max-parents", type=int, default=1 << 18)
+    ap.add_argument("--ring-gb", type=float, default=16.0)
+    ap.add_argument("--json", default=None, help="append a JSON run record to this file")
+    ap.add_argument("--csv-dir", default=".", help="directory of the CSV statistics files")
+    ap.add_argument("--no-csv", action="store_true")
+    return ap
+
+
+def _validate_pfsp(a) -> None:
+    def fail(msg):
+        sys.stderr.write(msg + "\n")
+        raise SystemExit(1)
+
+    if not 1 <= a.inst <= 120:
+        fail("Error: unsupported Taillard's instance")
+    if a.lb not in (0, 1, 2):
+        fail("Error: unsupported lower bound function")
+    if a.ub not in (0, 1):
+        fail("Error: unsupported upper bound initialization")
+    if a.m < 1:
+        fail("Error: unsupported minimal pool for GPU initialization")
+    if a.M < a.m:
+        fail("Error: unsupported maximal pool for GPU initialization")
+    if a.T < a.m:
+        fail("Error: unsupported maximal pool for CPU multi-core")
+    if a.D < 0:
+        fail("Error: unsupported number of GPU(s)")
+    if a.C < 0:
+        fail("Error: unsupported number of CPU Core(s)")
+    if a.ws not in (0, 1):
+        fail("Error: unsupported Intra-node Work Stealing option")
+    if a.L not in (0, 1):
+        fail("Error: unsupported distributed dynamic load balancing option")
+    if not 0 < a.perc <= 100:
+        fail("Error: unsupported WS percentage for popFrontBulkFree")
+
+
+def _rank_spec(a) -> dict:
+    return {"problem": "pfsp", "inst": a.inst, "lb": a.lb, "ub": a.ub, "backend": "gpu",
+            "engine": {"max_parents": a.max_parents, "ring_bytes": int(a.ring_gb * (1 << 30))},
+            "dist": {"m": a.m, "init_per_rank": a.m, "steal_cap": 5 * a.M, "ws": bool(a.ws), "L": bool(a.L)}}
+
+
+def pfsp_main(argv: list[str]) -> int:
+    a = _pfsp_parser().parse_args(argv)
+    _validate_pfsp(a)
+    from .models.pfsp import EngineOptions, PfspModel
+    from .search import solve_cpu, solve_engine
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    model = PfspModel(a.inst, a.lb)
+    if a.D == 0:
+        version = 0 if a.C <= 1 else 2
+        print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, 0, a.C, a.ws, 1, a.L, version))
+        r = solve_cpu(model, ub=a.ub, threads=a.C if a.C > 1 else 0, m=a.m, batch=20000, steal_cap=5 * a.M,
+                      ws=bool(a.ws), verbose=a.C > 1)
+        if a.C <= 1:
+            print("\nExploration terminated.")
+        print(report.pfsp_results(r.best, r.tree, r.sol, r.elapsed))
+        if not a.no_csv and a.C > 1:
+            report.write_multi_gpu_csv(os.path.join(a.csv_dir, "multigpu.csv"), a.inst, a.lb, 0, a.C, a.ws, r.best,
+                                       a.m, a.M, a.T, r.elapsed, r.tree, r.sol, r.workers)
+        _json(a, model, r, 0)
+        return 0
+
+    if a.D == 1 and world_env == 1:
+        print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, 1, a.C, a.ws, 1, a.L, 2))
+        eng = model.make_engine("gpu", 0, EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * 2**30)))
+        r = solve_engine(model, eng, ub=a.ub, m=a.m, verbose=True)
+        print(report.pfsp_results(r.best, r.tree, r.sol, r.elapsed))
+        if not a.no_csv:
+            w = r.workers[0]
+            report.write_single_gpu_csv(os.path.join(a.csv_dir, "singlegpu.csv"), a.inst, a.lb, r.best, a.m, a.M,
+                                        r.elapsed, w.t_memcpy, w.t_malloc, w.t_kernel, w.t_gen_child, r.tree, r.sol)
+            report.write_multi_gpu_csv(os.path.join(a.csv_dir, "multigpu.csv"), a.inst, a.lb, 1, 0, a.ws, r.best,
+                                       a.m, a.M, a.T, r.elapsed, r.tree, r.sol, r.workers)
+        _json(a, model, r, 1)
+        return 0
+
+    # ---- several GPUs: one process per GPU ----
+    from .parallel.workers import solve_rank
+
+    spec = _rank_spec(a)
+    if world_env > 1:  # already under torchrun
+        res = solve_rank(spec)
+        if res["rank"] != 0:
+            return 0
+    else:
+        from .ops import gpu_count
+        from .parallel.launch import spawn_local
+
+        if a.D > gpu_count():
+            print("Execution Terminated. More GPU devices requested than the ones available")
+            return 1
+        res = spawn_local(a.D, solve_rank, (spec,))[0]
+    D = res["world"]
+    print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, D, a.C, a.ws, 1, a.L, 2))
+    print(report.phase("Search on Parallel GPU completed", res["tree"], res["sol"], res["t_search"]))
+    print("\nExploration terminated.")
+    print(report.pfsp_results(res["best"], res["tree"], res["sol"], res["elapsed"]))
+    workers = [report.WorkerStats(**w) for w in res["workers"]]
+    if not a.no_csv:
+        report.write_multi_gpu_csv(os.path.join(a.csv_dir, "multigpu.csv"), a.inst, a.lb, D, 0, a.ws, res["best"],
+                                   a.m, a.M, a.T, res["elapsed"], res["tree"], res["sol"], workers)
+    if a.json:
+        report.write_json_record(a.json, {**model.describe(), "n_gpus": D, "tree": res["tree"], "sol": res["sol"],
+                                           "best": res["best"], "elapsed": res["elapsed"],
+                                           "nodes_per_sec": res["tree"] / max(res["elapsed"], 1e-12),
+                                           "rounds": res["extra"]["rounds"], "workers": res["workers"]})
+    return 0
+
+
+def _json(a, model, r, n_gpus) -> None:
+    if a.json:
+        from dataclasses import asdict
+
+        report.write_json_record(a.json, {**model.describe(), "n_gpus": n_gpus, "tree": r.tree, "sol": r.sol,
+                                          "best": r.best, "elapsed": r.elapsed, "nodes_per_sec": r.nodes_per_sec,
+                                          "workers": [asdict(w) for w in r.workers]})
+
+
+def nqueens_main(argv: list[str]) -> int:
+    ap = argparse.ArgumentParser(prog="nqueens", description="N-Queens backtracking")
+    ap.add_argument("-N", type=int, default=14)
+    ap.add_argument("-g", type=int, default=1)
+    ap.add_argument("-m", type=int, default=25)
+    ap.add_argument("-M", type=int, default=50000)
+    ap.add_argument("-D", type=int, default=1)
+    ap.add_argument("--max-parents", type=int, default=1 << 20)
+    a = ap.parse_args(argv)
+    for name, v in (("N", a.N), ("g", a.g), ("m", a.m)):
+        if v < 1:
+            sys.stderr.write(f"Error: {name} must be a positive integer.\n")
+            return 1
+    if a.M < a.m:
+        sys.stderr.write("Error: M must be a positive integer, greater or equal to m.\n")
+        return 1
+    from .models.nqueens import QueensModel
+    from .models.pfsp import EngineOptions
+    from .search import solve_cpu, solve_engine
+
+    model = QueensModel(a.N, a.g)
+    if a.D == 0:
+        print(report.queens_settings(a.N, a.g, "Sequential C++"))
+        r = solve_cpu(model)
+        print("\nExploration terminated.")
+        print(report.queens_results(r.tree, r.sol, r.elapsed))
+        return 0
+    if a.D == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        print(report.queens_settings(a.N, a.g, "Single-GPU C++/HIP (MI355X)"))
+        eng = model.make_engine("gpu", 0, EngineOptions(max_parents=a.max_parents))
+        r = solve_engine(model, eng, m=a.m, verbose=True)
+        print(report.queens_results(r.tree, r.sol, r.elapsed))
+        return 0
+    from .parallel.workers import solve_rank
+
+    spec = {"problem": "nqueens", "N": a.N, "G": a.g, "backend": "gpu",
+            "engine": {"max_parents": a.max_parents}, "dist": {"m": a.m, "init_per_rank": a.m}}
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        res = solve_rank(spec)
+        if res["rank"] != 0:
+            return 0
+    else:
+        from .parallel.launch import spawn_local
+
+        res = spawn_local(a.D, solve_rank, (spec,))[0]
+    print(report.queens_settings(a.N, a.g, f"Multi-GPU C++/HIP+RCCL ({res['world']} GPUs)"))
+    print(report.phase("Search on GPU completed", res["tree"], res["sol"], res["t_search"]))
+    print("\nExploration terminated.")
+    print(report.queens_results(res["tree"], res["sol"], res["elapsed"]))
+    return 0
+
+
+def main(argv: list[str] | None = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] not in ("pfsp", "nqueens"):
+        sys.stderr.write(__doc__ or "")
+        return 2
+    return pfsp_main(argv[1:]) if argv[0] == "pfsp" else nqueens_main(argv[1:])

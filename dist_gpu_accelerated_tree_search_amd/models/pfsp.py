@@ -1,0 +1,130 @@
+"""Permutation Flow-shop Scheduling (PFSP) problem model.
+
+Parity map (reference -> here):
+  c_taillard.c                      -> utils/taillard.py + csrc/core/taillard.hpp
+  c_bound_simple.c / c_bound_johnson.c (LB1, LB1_d, LB2)
+                                    -> csrc/core/pfsp_bounds_cpu.hpp (host oracle)
+                                       csrc/hip/pfsp_kernels.hpp     (gfx950 kernels)
+  PFSP_lib.c decompose_* / generate_children
+                                    -> csrc/core/problems.hpp (host) and the fused
+                                       expand kernel (device)
+  lb1_alloc_gpu / lb2_alloc_gpu     -> csrc/hip/pfsp_engine.hpp (tables owned by engine)
+
+A model instance is what a driver needs: the native instance, the bound kind,
+node layout, Step-1 warm-up / Step-3 drain on the host, and engine factories for
+the CPU and the GPU backends (same engine contract, csrc/core/engine_api.hpp).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .. import ops
+from ..utils import nodes as nodes_mod
+from ..utils import taillard as tl
+
+INT_MAX = 2**31 - 1
+
+
+@dataclass
+class EngineOptions:
+    max_parents: int = 1 << 18      # parents per device iteration (reference -M, sized for HBM)
+    ring_bytes: int = 16 << 30      # device pool capacity
+    iters_small: int = 6
+    iters_large: int = 48
+    use_graphs: bool = True
+    cpu_batch: int = 4096           # CPU engine batch
+    cpu_threads: int = 1
+
+
+class PfspModel:
+    kind = "pfsp"
+
+    def __init__(self, inst: int | None = 14, lb: int = 1, *, jobs: int | None = None, machines: int | None = None,
+                 p: np.ndarray | None = None, best_known: int | None = None):
+        if lb not in (0, 1, 2):
+            raise ValueError("lb must be 0 (LB1_d), 1 (LB1) or 2 (LB2)")
+        C = ops.cpu()
+        self.lb = lb
+        if p is None:
+            if inst is None:
+                raise ValueError("give a Taillard id or a processing-time matrix")
+            self.inst_id = int(inst)
+            self.native = C.PfspInstance.taillard(self.inst_id)
+        else:
+            p = np.asarray(p, dtype=np.int64)
+            if p.ndim != 2:
+                raise ValueError("p must be a (machines, jobs) matrix")
+            mm, n = p.shape
+            if (jobs is not None and jobs != n) or (machines is not None and machines != mm):
+                raise ValueError("jobs/machines do not match p")
+            self.inst_id = 0
+            self.native = C.PfspInstance.from_matrix(n, mm, p.reshape(-1).tolist(),
+                                                     INT_MAX if best_known is None else int(best_known))
+        self.jobs = self.native.jobs
+        self.machines = self.native.machines
+        self.best_known = self.native.best_known
+        self.node_bytes = nodes_mod.pfsp_node_bytes(self.jobs)
+
+    @classmethod
+    def synthetic(cls, jobs: int, machines: int, seed: int, lb: int = 1) -> "PfspModel":
+        return cls(None, lb, p=tl.synthetic(jobs, machines, seed))
+
+    # ---- incumbent ----
+    def initial_best(self, ub: int = 1) -> int:
+        """-u 1: best-known makespan (deterministic tree); -u 0: +inf."""
+        return self.best_known if ub == 1 else INT_MAX
+
+    # ---- host steps ----
+    def root(self) -> np.ndarray:
+        return nodes_mod.pfsp_root(self.jobs)
+
+    def warmup(self, best: int, target: int):
+        """Step 1 (ref pfsp_multigpu_cuda.c:111-118): breadth-first on the host until
+        `target` nodes. Returns (nodes, tree, sol, best)."""
+        return ops.cpu().pfsp_bfs(self.native, self.lb, int(best), int(target))
+
+    def drain(self, best: int, nodes: np.ndarray):
+        """Step 3 (ref :488-495): depth-first over leftovers. Returns (tree, sol, best)."""
+        return ops.cpu().pfsp_drain(self.native, self.lb, int(best), np.ascontiguousarray(nodes, dtype=np.uint8))
+
+    # ---- engines ----
+    def make_engine(self, backend: str = "gpu", device: int = 0, opts: EngineOptions | None = None):
+        opts = opts or EngineOptions()
+        if backend == "cpu":
+            return ops.cpu().make_pfsp_cpu_engine(self.native, self.lb, opts.cpu_batch, opts.cpu_threads)
+        if backend != "gpu":
+            raise ValueError(f"unknown backend {backend!r}")
+        H = ops.require_gpu(device)
+        return H.make_pfsp_engine(self.jobs, self.machines, list(self.native.p), self.lb, device=device,
+                                  max_parents=opts.max_parents, ring_bytes=opts.ring_bytes,
+                                  iters_small=opts.iters_small, iters_large=opts.iters_large,
+                                  use_graphs=opts.use_graphs, taillard_id=self.inst_id)
+
+    # ---- bounds (reference evaluate_gpu semantics; used by tests/tools) ----
+    def child_bounds_cpu(self, nodes: np.ndarray, best: int = INT_MAX) -> np.ndarray:
+        C = ops.cpu()
+        depths, perms = nodes_mod.pfsp_unpack(nodes, self.jobs)
+        out = []
+        for d, q in zip(depths, perms):
+            d = int(d)
+            if self.lb == 0:
+                by_job = C.lb1_children(self.native, q.tolist(), d)
+                out.extend(by_job[int(q[k])] for k in range(d, self.jobs))
+                continue
+            for k in range(d, self.jobs):
+                c = q.copy()
+                c[d], c[k] = c[k], c[d]
+                out.append(C.lb1(self.native, c.tolist(), d + 1) if self.lb == 1 else
+                           C.lb2(self.native, c.tolist(), d + 1, int(best)))
+        return np.asarray(out, dtype=np.int64)
+
+    def child_bounds_gpu(self, nodes: np.ndarray, best: int = INT_MAX, device: int = 0) -> np.ndarray:
+        H = ops.require_gpu(device)
+        return H.pfsp_bounds(self.jobs, self.machines, list(self.native.p), self.lb,
+                             np.ascontiguousarray(nodes, dtype=np.uint8), int(best), device)
+
+    def describe(self) -> dict:
+        return {"problem": "pfsp", "inst": self.inst_id, "jobs": self.jobs, "machines": self.machines, "lb": self.lb,
+                "best_known": self.best_known}

@@ -1,0 +1,219 @@
+"""torch.distributed transport for the tree-search runtime (RCCL on MI355X, gloo on CPU).
+
+One process per GPU. The reference moves work between GPUs through host memory
+under OpenMP spin locks (ref pfsp_multigpu_cuda.c:343-431) and between nodes with
+MPI Allgather/Allgatherv of every donor's nodes (ref pfsp_dist_multigpu_cuda.c:
+122-137, 364-469). Here every exchange is a collective or a targeted point-to-point
+transfer issued by all ranks in the same order:
+  * status round      one all_gather of a small int64 record per rank
+                      (pool size, incumbent, idle flag) — replaces the separate
+                      Allreduce(best) + Allgather(termination) + Allgather(needs)
+  * work transfer     batch_isend_irecv donor -> needy only, straight from the
+                      device pool (engine.export_to) into the peer's pool over xGMI;
+                      never an all-gather of everybody's nodes.
+  * final reduction   all_reduce SUM of counters / MIN of the incumbent.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+@dataclass
+class Topology:
+    rank: int
+    world: int
+    local_rank: int
+    local_world: int
+
+    @property
+    def node(self) -> int:
+        return self.rank // max(1, self.local_world)
+
+
+class Comm:
+    """Process-group wrapper; world == 1 works without any process group."""
+
+    def __init__(self, backend: str | None = None, use_gpu: bool = True, timeout_s: float = 1800.0):
+        import torch
+        import torch.distributed as dist
+
+        self.torch = torch
+        self.dist = dist
+        self.topo = Topology(rank=_env_int("RANK", 0), world=_env_int("WORLD_SIZE", 1),
+                             local_rank=_env_int("LOCAL_RANK", 0),
+                             local_world=_env_int("LOCAL_WORLD_SIZE", _env_int("WORLD_SIZE", 1)))
+        self.use_gpu = use_gpu
+        if use_gpu:
+            torch.cuda.set_device(self.topo.local_rank)
+            self.device = torch.device("cuda", self.topo.local_rank)
+        else:
+            self.device = torch.device("cpu")
+        self.backend = backend or ("nccl" if use_gpu else "gloo")
+        self._owns_pg = False
+        if self.topo.world > 1 and not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kw = dict(backend=self.backend, timeout=datetime.timedelta(seconds=timeout_s))
+            if use_gpu and self.backend == "nccl":
+                kw["device_id"] = self.device
+            dist.init_process_group(**kw)
+            self._owns_pg = True
+        self._buf = None
+        self.bytes_sent = 0
+        self.bytes_recv = 0
+
+    # ---- basic properties ----
+    @property
+    def rank(self) -> int:
+        return self.topo.rank
+
+    @property
+    def world(self) -> int:
+        return self.topo.world
+
+    @property
+    def distributed(self) -> bool:
+        return self.topo.world > 1
+
+    def sync_device(self) -> None:
+        if self.use_gpu:
+            self.torch.cuda.synchronize(self.device)
+
+    def barrier(self) -> None:
+        if self.distributed:
+            if self.use_gpu and self.backend == "nccl":
+                self.dist.barrier(device_ids=[self.topo.local_rank])
+            else:
+                self.dist.barrier()
+        self.sync_device()
+
+    def close(self) -> None:
+        if self._owns_pg and self.dist.is_initialized():
+            self.dist.destroy_process_group()
+            self._owns_pg = False
+
+    # ---- collectives on small int64 records ----
+    def allgather_i64(self, values) -> np.ndarray:
+        vals = np.asarray(values, dtype=np.int64).reshape(-1)
+        if not self.distributed:
+            return vals.reshape(1, -1)
+        t = self.torch.as_tensor(vals, dtype=self.torch.int64).to(self.device)
+        out = self.torch.empty(self.world * vals.size, dtype=self.torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t)
+        return out.cpu().numpy().reshape(self.world, vals.size)
+
+    def allreduce_i64(self, values, op: str = "sum") -> np.ndarray:
+        vals = np.asarray(values, dtype=np.int64).reshape(-1)
+        if not self.distributed:
+            return vals
+        t = self.torch.as_tensor(vals, dtype=self.torch.int64).to(self.device)
+        rop = {"sum": self.dist.ReduceOp.SUM, "min": self.dist.ReduceOp.MIN, "max": self.dist.ReduceOp.MAX}[op]
+        self.dist.all_reduce(t, op=rop)
+        return t.cpu().numpy()
+
+    def allgather_f64(self, values) -> np.ndarray:
+        vals = np.asarray(values, dtype=np.float64).reshape(-1)
+        if not self.distributed:
+            return vals.reshape(1, -1)
+        t = self.torch.as_tensor(vals, dtype=self.torch.float64).to(self.device)
+        out = self.torch.empty(self.world * vals.size, dtype=self.torch.float64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t)
+        return out.cpu().numpy().reshape(self.world, vals.size)
+
+    # ---- node transfers ----
+    def _buffer(self, nbytes: int):
+        if self._buf is None or self._buf.numel() < nbytes:
+            cap = max(nbytes, 1 << 20)
+            self._buf = self.torch.empty(cap, dtype=self.torch.uint8, device=self.device)
+        return self._buf
+
+    def execute_transfers(self, plan, engine, node_bytes: int) -> tuple[int, int]:
+        """Run the planned (donor, receiver, count) transfers. Every rank calls this
+        with the same plan. Returns (nodes_sent, nodes_received) for this rank.
+
+        GPU comm (RCCL): nodes go device pool -> device buffer -> xGMI -> peer buffer
+        -> peer pool, never touching host memory. CPU comm (gloo): nodes are staged
+        through host arrays (this also lets GPU engines share one device in tests)."""
+        me = self.rank
+        outgoing = [(r, k) for (d, r, k) in plan if d == me and k > 0]
+        incoming = [(d, k) for (d, r, k) in plan if r == me and k > 0]
+        if not outgoing and not incoming:
+            return 0, 0
+        total_out = sum(k for _, k in outgoing)
+        total_in = sum(k for _, k in incoming)
+        torch = self.torch
+        on_device = self.device.type != "cpu"
+        ops = []
+        if on_device:
+            buf = self._buffer(max(total_out, total_in) * node_bytes)
+            if outgoing:
+                got = engine.export_to(buf.data_ptr(), total_out)
+                if got != total_out:
+                    raise RuntimeError(f"rank {me}: planned to send {total_out} nodes, pool gave {got}")
+            src = buf
+            dst = buf
+        else:
+            src = None
+            if outgoing:
+                host = engine.pop(total_out)
+                if len(host) != total_out:
+                    raise RuntimeError(f"rank {me}: planned to send {total_out} nodes, pool gave {len(host)}")
+                src = torch.from_numpy(np.ascontiguousarray(host).reshape(-1))
+            dst = torch.empty(total_in * node_bytes, dtype=torch.uint8) if incoming else None
+        off = 0
+        for r, k in outgoing:
+            ops.append(self.dist.P2POp(self.dist.isend, src[off * node_bytes:(off + k) * node_bytes], r))
+            off += k
+        off = 0
+        for d, k in incoming:
+            ops.append(self.dist.P2POp(self.dist.irecv, dst[off * node_bytes:(off + k) * node_bytes], d))
+            off += k
+        for w in self.dist.batch_isend_irecv(ops):
+            w.wait()
+        if incoming:
+            if on_device:
+                self.sync_device()
+                engine.import_from(dst.data_ptr(), total_in)
+            else:
+                engine.push(dst.numpy().reshape(total_in, node_bytes))
+        self.bytes_sent += total_out * node_bytes
+        self.bytes_recv += total_in * node_bytes
+        return total_out, total_in
+
+
+def plan_sharing(sizes, m: int, cap: int, node_of=None, intra: bool = True, inter: bool = True):
+    """Deterministic steal-half matching computed identically on every rank.
+
+    needy  = ranks whose pool holds fewer than m nodes (ref popBackBulk threshold),
+    donors = ranks with at least 2m nodes (ref steal condition `size >= 2*m`).
+    Each needy rank is served by the donor with the most nodes left, which hands
+    over half of what it has (capped at `cap`, ref 5*M). intra/inter restrict pairs
+    to the same node (-w) or to different nodes (-L)."""
+    sizes = [int(s) for s in sizes]
+    n = len(sizes)
+    node_of = node_of or (lambda r: 0)
+    left = list(sizes)
+    needy = [r for r in range(n) if sizes[r] < m]
+    needy_set = set(needy)
+    plan = []
+    for r in needy:
+        cands = [d for d in range(n) if left[d] >= 2 * m and d not in needy_set and
+                 ((intra and node_of(d) == node_of(r)) or (inter and node_of(d) != node_of(r)))]
+        if not cands:
+            continue
+        d = max(cands, key=lambda x: (left[x], -x))
+        k = min(left[d] // 2, cap)
+        if k <= 0:
+            continue
+        left[d] -= k
+        left[r] += k
+        plan.append((d, r, k))
+    return plan

@@ -1,0 +1,142 @@
+"""Distributed B&B runtime: one process (= one engine) per GPU, lock-step rounds.
+
+Parity with the reference's two parallel engines:
+  * intra-node multi-GPU (ref pfsp_multigpu_cuda.c): Step 1 BFS to workers*m nodes,
+    round-robin split (roundRobin_distribution), per-GPU pools, random steal-half
+    work stealing, BUSY/IDLE termination, incumbent sharing (checkBest);
+  * distributed multi-node (ref pfsp_dist_multigpu_cuda.c): redundant Step 1 on
+    every rank + rank-strided share, a comm thread doing Allreduce(best) /
+    Allgather(termination, needs_work) / Allgatherv(nodes) rounds (DWS, -L 1) or a
+    static partition (-L 0), final reductions.
+
+Here every rank runs the same loop:
+    run its device pool for a time slice (fused kernels, no host round trips)
+    -> one status all_gather {pool size, incumbent}
+    -> incumbent = MIN over ranks          (replaces checkBest + Allreduce MIN)
+    -> all pools empty => terminate        (exact: no node is in flight between rounds)
+    -> steal-half plan, identical on all ranks, executed as targeted
+       device-to-device transfers (replaces spin-lock steals and Allgatherv).
+The slice adapts: it doubles while no rank is starving and resets when one is.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..search import SolveResult
+from ..utils.report import WorkerStats
+from .comm import Comm, plan_sharing
+
+
+@dataclass
+class DistConfig:
+    m: int = 25                  # needy below m nodes; donors need >= 2m (ref -m)
+    init_per_rank: int = 25      # Step-1 nodes per rank (ref: workers * m)
+    steal_cap: int = 250_000     # max nodes per transfer (ref 5*M)
+    slice_min_s: float = 0.0005  # local work between rounds (adaptive)
+    slice_max_s: float = 0.050
+    ws: bool = True              # share within a node (ref -w)
+    L: bool = True               # share across nodes (ref -L)
+    verbose: bool = False
+
+
+@dataclass
+class RankStats:
+    tree: int = 0
+    sol: int = 0
+    rounds: int = 0
+    sent: int = 0
+    received: int = 0
+    transfers_in: int = 0
+    transfers_out: int = 0
+    t_run: float = 0.0
+    t_comm: float = 0.0
+    t_idle: float = 0.0
+    t_init: float = 0.0
+
+
+def round_robin_share(n: int, rank: int, world: int) -> np.ndarray:
+    """Indices rank, rank+world, ... ; the last rank also takes the tail
+    (ref Pool_atom.c:14-36 roundRobin_distribution)."""
+    c = n // world
+    idx = rank + world * np.arange(c)
+    if rank == world - 1:
+        idx = np.concatenate([idx, np.arange(world * c, n)])
+    return idx.astype(np.int64)
+
+
+def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | None = None) -> SolveResult:
+    """Cooperative solve of `model` by all ranks of `comm`; returns the global result
+    (identical on every rank) with per-rank WorkerStats in `workers`."""
+    cfg = cfg or DistConfig()
+    rs = RankStats()
+    world, rank = comm.world, comm.rank
+    t_start = time.perf_counter()
+
+    # ---- Step 1: redundant, deterministic host warm-up on every rank ----
+    best = model.initial_best(ub)
+    nodes, tree1, sol1, best = model.warmup(best, world * cfg.init_per_rank)
+    mine = nodes[round_robin_share(len(nodes), rank, world)]
+    engine.reset_counters()
+    engine.best = int(best)
+    if len(mine):
+        engine.push(np.ascontiguousarray(mine))
+    rs.t_init = time.perf_counter() - t_start
+
+    # ---- Step 2: rounds ----
+    share = cfg.ws or cfg.L
+    node_of = lambda r: r // max(1, comm.topo.local_world)  # noqa: E731
+    slice_s = cfg.slice_min_s
+    t_loop = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        engine.run(max_seconds=slice_s, stop_below=1)
+        t1 = time.perf_counter()
+        rs.t_run += t1 - t0
+        size = engine.size()
+        st = comm.allgather_i64([size, engine.best])
+        rs.rounds += 1
+        gbest = int(st[:, 1].min())
+        if gbest < engine.best:
+            engine.best = gbest
+        sizes = st[:, 0]
+        if int(sizes.sum()) == 0:
+            rs.t_comm += time.perf_counter() - t1
+            break
+        starving = bool((sizes < cfg.m).any())
+        if share and world > 1 and starving:
+            plan = plan_sharing(sizes, cfg.m, cfg.steal_cap, node_of, intra=cfg.ws, inter=cfg.L)
+            if plan:
+                sent, got = comm.execute_transfers(plan, engine, model.node_bytes)
+                rs.sent += sent
+                rs.received += got
+                rs.transfers_out += sum(1 for d, _, _ in plan if d == rank)
+                rs.transfers_in += sum(1 for _, r, _ in plan if r == rank)
+            slice_s = cfg.slice_min_s
+        else:
+            slice_s = min(cfg.slice_max_s, slice_s * 2)
+        if size == 0:
+            rs.t_idle += time.perf_counter() - t0
+        rs.t_comm += time.perf_counter() - t1
+    t_search = time.perf_counter() - t_loop
+
+    # ---- Step 3 (nothing left by construction) + reductions ----
+    st = engine.stats()
+    rs.tree, rs.sol = int(st["tree"]), int(st["sol"])
+    best_local = min(int(st["best"]), int(best))
+    tot = comm.allreduce_i64([rs.tree + (tree1 if rank == 0 else 0), rs.sol + (sol1 if rank == 0 else 0)], "sum")
+    gbest = int(comm.allreduce_i64([best_local], "min")[0])
+    per = comm.allgather_f64([rs.tree, rs.sol, rs.sent, rs.received, rs.transfers_in, rs.transfers_out,
+                              rs.rounds, rs.t_run, rs.t_comm, rs.t_idle, rs.t_init,
+                              float(st.get("t_memcpy", 0.0)), float(st.get("t_malloc", 0.0))])
+    elapsed = time.perf_counter() - t_start
+    workers = [WorkerStats(tree=int(r[0]), sol=int(r[1]), gen_child=int(r[0]), steals=int(r[4]),
+                           success_steals=int(r[4]), terminations=int(r[6]), t_memcpy=float(r[11]),
+                           t_malloc=float(r[12]), t_kernel=float(r[7]), t_pool_ops=float(r[8]),
+                           t_idle=float(r[9]), t_termination=0.0) for r in per]
+    return SolveResult(best=gbest, tree=int(tot[0]), sol=int(tot[1]), elapsed=elapsed, t_init=rs.t_init,
+                       t_search=t_search, t_tail=0.0, workers=workers,
+                       extra={"rounds": rs.rounds, "sent_nodes": [int(r[2]) for r in per],
+                              "received_nodes": [int(r[3]) for r in per], "world": world})

@@ -1,0 +1,43 @@
+"""Rank entry points (picklable, importable) for launchers, tests and the CLI."""
+from __future__ import annotations
+
+from dataclasses import asdict
+
+from ..models.nqueens import QueensModel
+from ..models.pfsp import EngineOptions, PfspModel
+from .comm import Comm
+from .runtime import DistConfig, distributed_solve
+
+
+def build_model(spec: dict):
+    if spec.get("problem", "pfsp") == "pfsp":
+        if spec.get("synthetic"):
+            j, mm, seed = spec["synthetic"]
+            return PfspModel.synthetic(j, mm, seed, lb=spec.get("lb", 1))
+        return PfspModel(spec.get("inst", 14), spec.get("lb", 1))
+    return QueensModel(spec.get("N", 14), spec.get("G", 1))
+
+
+def solve_rank(spec: dict) -> dict:
+    """Solve spec's problem cooperatively on all ranks of the current process group."""
+    backend = spec.get("backend", "gpu")
+    # comm on the GPU (RCCL) unless asked for gloo, e.g. several ranks sharing one GPU
+    comm = Comm(use_gpu=(backend == "gpu" and spec.get("comm", "nccl") == "nccl"))
+    try:
+        model = build_model(spec)
+        opts = EngineOptions(**spec.get("engine", {}))
+        device = int(spec.get("device", comm.topo.local_rank)) if backend == "gpu" else 0
+        engine = model.make_engine(backend, device, opts)
+        cfg = DistConfig(**spec.get("dist", {}))
+        res = None
+        for _ in range(int(spec.get("repeat", 1))):
+            comm.barrier()
+            res = distributed_solve(model, engine, comm, ub=spec.get("ub", 1), cfg=cfg)
+        out = {"rank": comm.rank, "world": comm.world, "best": res.best, "tree": res.tree, "sol": res.sol,
+               "elapsed": res.elapsed, "t_init": res.t_init, "t_search": res.t_search, "extra": res.extra,
+               "workers": [asdict(w) for w in res.workers]}
+        del engine
+        return out
+    finally:
+        comm.barrier()
+        comm.close()

@@ -1,0 +1,104 @@
+"""Single-process search drivers (CPU sequential, CPU multi-core, one GPU).
+
+The three-step structure of every reference driver is kept
+(ref pfsp_multigpu_cuda.c:55-511, nqueens_gpu_cuda.cu:198-264):
+  Step 1  host breadth-first warm-up until the pool holds `m` (x workers) nodes,
+  Step 2  the parallel / device search,
+  Step 3  host depth-first drain of whatever Step 2 leaves (nothing, on the GPU
+          path: the device engine drains its pool completely).
+Counting (tree / sol) and the -u incumbent rule are the reference's.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import ops
+from .models.pfsp import EngineOptions
+from .utils.report import WorkerStats
+
+
+@dataclass
+class SolveResult:
+    best: int
+    tree: int
+    sol: int
+    elapsed: float
+    t_init: float = 0.0
+    t_search: float = 0.0
+    t_tail: float = 0.0
+    workers: list = field(default_factory=list)
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def nodes_per_sec(self) -> float:
+        return self.tree / self.elapsed if self.elapsed > 0 else float("inf")
+
+
+def solve_cpu(model, ub: int = 1, threads: int = 0, m: int = 25, batch: int = 20000, steal_cap: int = 250000,
+              ws: bool = True, verbose: bool = False) -> SolveResult:
+    """threads == 0: sequential (ref pfsp_c.c / nqueens_c.c); >0: multi-core WS
+    (ref pfsp_omp_c.c)."""
+    C = ops.cpu()
+    if model.kind == "pfsp":
+        r = C.run_pfsp(model.native, model.lb, model.initial_best(ub), threads=threads, m=m, batch=batch,
+                       steal_cap=steal_cap, ws=ws, verbose=verbose)
+    else:
+        r = C.run_queens(model.N, model.G, threads=threads, m=m, batch=batch, steal_cap=steal_cap, ws=ws,
+                         verbose=verbose)
+    return SolveResult(best=r["best"], tree=r["tree"], sol=r["sol"], elapsed=r["elapsed"], t_init=r["t_init"],
+                       t_search=r["t_search"], t_tail=r["t_tail"],
+                       workers=[WorkerStats.from_dict(w) for w in r["workers"]])
+
+
+def solve_engine(model, engine, ub: int = 1, m: int = 25, best: int | None = None,
+                 verbose: bool = False) -> SolveResult:
+    """One complete solve on an existing engine (GPU or CPU backend).
+
+    The engine is reused across solves (allocation and graph capture are setup,
+    like model initialisation); its counters are reset here."""
+    t0 = time.perf_counter()
+    best = model.initial_best(ub) if best is None else best
+    nodes, tree1, sol1, best = model.warmup(best, m)
+    t1 = time.perf_counter()
+    if verbose:
+        from .utils.report import phase
+        print(phase("Initial search on CPU completed", tree1, sol1, t1 - t0))
+    engine.reset_counters()
+    engine.best = int(best)
+    engine.push(nodes)
+    launches = engine.run()
+    st = engine.stats()
+    best = min(best, st["best"])
+    t2 = time.perf_counter()
+    tree, sol = tree1 + st["tree"], sol1 + st["sol"]
+    if verbose:
+        print(phase("Search on GPU completed", tree, sol, t2 - t1))
+    # Step 3: the engine drains completely; anything left (none) goes to the host
+    left = engine.size()
+    if left:
+        rest = engine.pop(left)
+        tr, so, best = model.drain(best, rest)
+        tree += tr
+        sol += so
+    t3 = time.perf_counter()
+    if verbose:
+        print(phase("Final on CPU completed", tree, sol, t3 - t2))
+        print("\nExploration terminated.")
+    w = WorkerStats(tree=st["tree"], sol=st["sol"], gen_child=st["tree"], t_memcpy=st["t_memcpy"],
+                    t_malloc=st["t_malloc"], t_kernel=st["t_run"])
+    return SolveResult(best=best, tree=tree, sol=sol, elapsed=t3 - t0, t_init=t1 - t0, t_search=t2 - t1,
+                       t_tail=t3 - t2, workers=[w], extra={"launches": launches, "iters": st["iters"],
+                                                           "parents": st["parents"], "syncs": st["syncs"]})
+
+
+def solve_gpu(model, ub: int = 1, device: int = 0, m: int = 25, opts: EngineOptions | None = None,
+              verbose: bool = False) -> SolveResult:
+    """Single-GPU solve (ref pfsp_multigpu_cuda.c with -D 1 -C 0)."""
+    eng = model.make_engine("gpu", device, opts)
+    try:
+        return solve_engine(model, eng, ub=ub, m=m, verbose=verbose)
+    finally:
+        del eng

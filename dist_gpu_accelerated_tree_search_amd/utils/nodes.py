@@ -1,0 +1,68 @@
+"""numpy views of the node layouts shared by host and device pools.
+
+PFSP node (csrc/core/pfsp_node.hpp): id_t depth; id_t prmu[NJ]; padded to 16 B,
+id_t = uint8 for NJ <= 255 else uint16. N-Queens node: 4 x uint32
+{cols, diag, anti, depth}. Parity: ref pfsp/lib/PFSP_node.h:15-20 (44-B node with
+limit1 stored), nqueens/lib/NQueens_node.h:13-17 (board).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+BUCKETS = (20, 50, 100, 200, 500)
+
+
+def pfsp_bucket(jobs: int) -> int:
+    for b in BUCKETS:
+        if jobs <= b:
+            return b
+    return 500
+
+
+def pfsp_id_dtype(jobs: int):
+    return np.uint16 if pfsp_bucket(jobs) > 255 else np.uint8
+
+
+def pfsp_node_bytes(jobs: int) -> int:
+    nj = pfsp_bucket(jobs)
+    isz = np.dtype(pfsp_id_dtype(jobs)).itemsize
+    raw = (nj + 1) * isz
+    return (raw + 15) // 16 * 16
+
+
+def pfsp_pack(depths, perms, jobs: int) -> np.ndarray:
+    """Pack (depth, permutation) pairs into an (n, node_bytes) uint8 array."""
+    depths = np.asarray(depths)
+    perms = np.asarray(perms)
+    n = len(depths)
+    nb = pfsp_node_bytes(jobs)
+    dt = pfsp_id_dtype(jobs)
+    isz = np.dtype(dt).itemsize
+    out = np.zeros((n, nb // isz), dtype=dt)
+    out[:, 0] = depths
+    out[:, 1 : 1 + jobs] = perms
+    return out.view(np.uint8).reshape(n, nb)
+
+
+def pfsp_unpack(nodes: np.ndarray, jobs: int):
+    """Inverse of pfsp_pack: (depths[n], perms[n, jobs])."""
+    dt = pfsp_id_dtype(jobs)
+    v = np.ascontiguousarray(nodes).view(dt)
+    return v[:, 0].astype(np.int64), v[:, 1 : 1 + jobs].astype(np.int64)
+
+
+def pfsp_root(jobs: int) -> np.ndarray:
+    return pfsp_pack([0], [np.arange(jobs)], jobs)
+
+
+QUEENS_NODE_BYTES = 16
+
+
+def queens_pack(cols, diag, anti, depth) -> np.ndarray:
+    a = np.stack([np.asarray(cols), np.asarray(diag), np.asarray(anti), np.asarray(depth)], axis=1).astype(np.uint32)
+    return a.view(np.uint8).reshape(len(a), QUEENS_NODE_BYTES)
+
+
+def queens_unpack(nodes: np.ndarray):
+    v = np.ascontiguousarray(nodes).view(np.uint32).reshape(-1, 4)
+    return v[:, 0], v[:, 1], v[:, 2], v[:, 3]

@@ -1,0 +1,80 @@
+"""Distributed runtime on CPU ranks over gloo (torch.distributed), world 2-4.
+
+The reference has no loopback harness; here the same round protocol
+(status all_gather, incumbent MIN, steal-half plan, point-to-point transfers,
+termination) runs with CPU engines, so lost or duplicated nodes show up as a wrong
+golden tree."""
+import pytest
+
+from dist_gpu_accelerated_tree_search_amd.parallel.comm import plan_sharing
+from dist_gpu_accelerated_tree_search_amd.parallel.launch import spawn_local
+from dist_gpu_accelerated_tree_search_amd.parallel.runtime import round_robin_share
+from dist_gpu_accelerated_tree_search_amd.parallel.workers import solve_rank
+
+GOLD = (2573652, 2648, 1377)
+
+
+def test_round_robin_share_partitions():
+    for n in (0, 1, 7, 25, 100, 101):
+        for world in (1, 2, 3, 8):
+            parts = [round_robin_share(n, r, world) for r in range(world)]
+            allidx = sorted(int(i) for p in parts for i in p)
+            assert allidx == list(range(n))
+            # reference: element i goes to worker i % world, tail to the last worker
+            c = n // world
+            for r in range(world - 1):
+                assert list(parts[r]) == [r + world * t for t in range(c)]
+
+
+def test_plan_sharing_properties():
+    plan = plan_sharing([0, 1000, 0, 10], m=25, cap=10_000)
+    assert plan == [(1, 0, 500), (1, 2, 250), (1, 3, 125)]
+    assert plan_sharing([30, 40, 50], m=25, cap=100) == []          # nobody starving
+    assert plan_sharing([0, 40], m=25, cap=100) == []               # donor below 2m
+    assert plan_sharing([0, 10_000], m=25, cap=100) == [(1, 0, 100)]  # capped (ref 5*M)
+    # intra-node only: ranks 0,1 on node 0 and 2,3 on node 1
+    node_of = lambda r: r // 2  # noqa: E731
+    p = plan_sharing([0, 1000, 0, 0], 25, 10_000, node_of, intra=True, inter=False)
+    assert p == [(1, 0, 500)]
+    p = plan_sharing([0, 1000, 0, 0], 25, 10_000, node_of, intra=False, inter=True)
+    assert [x[:2] for x in p] == [(1, 2), (1, 3)]
+    # a receiver is never asked to donate in the same round
+    p = plan_sharing([0, 100, 0], 25, 10_000)
+    assert all(d == 1 for d, _, _ in p)
+
+
+@pytest.mark.parametrize("world,ws,lb", [(2, True, 0), (3, True, 1), (4, True, 0), (3, False, 0)])
+def test_pfsp_golden_tree(world, ws, lb):
+    spec = {"problem": "pfsp", "inst": 14, "lb": lb, "backend": "cpu", "dist": {"ws": ws, "L": ws}}
+    res = spawn_local(world, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == GOLD
+    per_rank = [w["tree"] for w in res[0]["workers"]]
+    assert len(per_rank) == world and all(t > 0 for t in per_rank)
+    if ws:
+        assert sum(res[0]["extra"]["sent_nodes"]) == sum(res[0]["extra"]["received_nodes"])
+
+
+def test_pfsp_lb2_and_unknown_optimum():
+    spec = {"problem": "pfsp", "inst": 3, "lb": 2, "backend": "cpu", "ub": 1}
+    res = spawn_local(2, solve_rank, (spec,), timeout=300)
+    assert (res[0]["tree"], res[0]["sol"], res[0]["best"]) == (80062, 0, 1081)
+    spec = {"problem": "pfsp", "synthetic": (9, 5, 77), "lb": 1, "backend": "cpu", "ub": 0}
+    res = spawn_local(3, solve_rank, (spec,), timeout=300)
+    from dist_gpu_accelerated_tree_search_amd import PfspModel, solve_cpu
+
+    assert res[0]["best"] == solve_cpu(PfspModel.synthetic(9, 5, 77, lb=1), ub=0).best
+
+
+def test_queens_and_stress_small_thresholds():
+    spec = {"problem": "nqueens", "N": 11, "backend": "cpu",
+            "engine": {"cpu_batch": 64}, "dist": {"m": 4, "init_per_rank": 2, "slice_min_s": 0.0001}}
+    res = spawn_local(4, solve_rank, (spec,), timeout=300)
+    assert (res[0]["tree"], res[0]["sol"]) == (166925, 2680)
+    assert res[0]["extra"]["rounds"] > 1
+
+
+def test_repeated_solves_reuse_engine():
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu", "repeat": 3}
+    res = spawn_local(2, solve_rank, (spec,), timeout=300)
+    assert (res[1]["tree"], res[1]["sol"], res[1]["best"]) == GOLD

@@ -1,0 +1,83 @@
+"""Device engine end to end: golden trees, pool management (spill/refill), export/import."""
+import numpy as np
+import pytest
+
+from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel, QueensModel, solve_engine, solve_gpu
+from dist_gpu_accelerated_tree_search_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = {(14, 0): (2573652, 2648, 1377), (14, 1): (2573652, 2648, 1377), (14, 2): (144639, 0, 1377),
+          (3, 1): (2573133, 5689, 1081), (3, 2): (80062, 0, 1081), (4, 1): (1163892, 941, 1293),
+          (7, 0): (271602, 28447, 1234), (11, 2): (438563, 0, 1582), (12, 0): (3913907, 18, 1659),
+          (13, 1): (4052758, 15, 1496), (16, 2): (2646205, 0, 1397), (2, 2): (7, 0, 1359)}
+SMALL = EngineOptions(ring_bytes=1 << 30)
+
+
+@pytest.mark.parametrize("key", sorted(GOLDEN))
+def test_pfsp_golden_on_gpu(key):
+    r = solve_gpu(PfspModel(*key), ub=1, opts=SMALL)
+    assert (r.tree, r.sol, r.best) == GOLDEN[key]
+
+
+def test_pfsp_bigger_trees_on_gpu():
+    # ta008 LB1_d: 113,458,723 nodes (20 s sequential in the reference); ta010 LB2: 8,122,579
+    r = solve_gpu(PfspModel(8, 0), opts=SMALL)
+    assert (r.tree, r.sol, r.best) == (113458723, 808498, 1206)
+    r = solve_gpu(PfspModel(10, 2), opts=SMALL)
+    assert (r.tree, r.sol, r.best) == (8122579, 0, 1108)
+
+
+@pytest.mark.parametrize("N,gold", [(8, (2056, 92)), (12, (856188, 14200)), (14, (27358552, 365596)),
+                                    (15, (171129071, 2279184))])
+def test_queens_golden_on_gpu(N, gold):
+    r = solve_gpu(QueensModel(N), opts=EngineOptions(max_parents=1 << 20, ring_bytes=2 << 30))
+    assert (r.tree, r.sol) == gold
+
+
+def test_engine_reuse_graphs_off_and_small_windows():
+    model = PfspModel(14, 1)
+    for opts in (EngineOptions(max_parents=1 << 12, ring_bytes=1 << 28, use_graphs=False),
+                 EngineOptions(max_parents=1 << 10, ring_bytes=1 << 20, iters_large=12)):  # tiny ring: spills
+        eng = model.make_engine("gpu", 0, opts)
+        for _ in range(2):
+            r = solve_engine(model, eng)
+            assert (r.tree, r.sol, r.best) == GOLDEN[(14, 1)]
+
+
+def test_spill_and_refill_with_unknown_optimum():
+    # -u 0 grows a much larger pool; a 1-MB ring forces host spill + refill
+    model = PfspModel(14, 0)
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=1 << 20, iters_large=12))
+    r = solve_engine(model, eng, ub=0)
+    st = eng.stats()
+    assert r.best == 1377
+    assert st["spilled"] > 0 and st["refilled"] > 0
+
+
+def test_push_pop_export_import_roundtrip():
+    import torch
+
+    model = PfspModel(14, 1)
+    C = ops.cpu()
+    nodes, tree1, sol1, best = C.pfsp_bfs(model.native, 1, 1377, 500)
+    eng = model.make_engine("gpu", 0, SMALL)
+    eng.best = 1377
+    eng.push(nodes)
+    assert eng.size() == len(nodes)
+    back = eng.pop(100)
+    assert back.shape == (100, 32)
+    buf = torch.empty(200 * 32, dtype=torch.uint8, device="cuda:0")
+    n = eng.export_to(buf.data_ptr(), 200)
+    assert n == 200 and eng.size() == len(nodes) - 300
+    torch.cuda.synchronize()
+    # nodes come back intact: export/pop return a subset of what was pushed
+    pushed = {bytes(r) for r in nodes}
+    assert all(bytes(r) in pushed for r in back)
+    assert all(bytes(r) in pushed for r in buf.cpu().numpy().reshape(200, 32))
+    eng.import_from(buf.data_ptr(), 200)
+    eng.push(back)
+    assert eng.size() == len(nodes)
+    eng.run()
+    st = eng.stats()
+    assert (st["tree"] + tree1, st["sol"] + sol1) == (2573652, 2648)
