@@ -24,14 +24,8 @@ using u64 = unsigned long long;
 constexpr int kWave = 64;      // CDNA wavefront width
 constexpr int kBlock = 256;    // 4 waves per workgroup for every search kernel
 
-// Pool control block (device memory). The device-resident pool is
-//   * a ring-buffer stack  ring[(bot + i) & mask], i < stack[s]
-//   * plus the children buffer written by the previous iteration, bufs[t%2][0..buf[s])
-// Iteration t of a launch sequence reads slot t%3, accumulates into slot (t+1)%3 and
-// clears slot (t+2)%3 (the one read by iteration t-1), so consecutive kernels never
-// race on a counter, with no per-iteration host work and no extra launch.
-// Every field that device atomics touch sits on its own 128-B line, apart from the
-// fields that are plain-stored, so a plain write-back never merges with an atomic.
+// 128-B padded scalars: a plain write-back of one never merges with another's
+// line (the incumbent is the only word updated by device atomics).
 struct alignas(128) CtlU64 {
   u64 v;
   u64 pad[15];
@@ -39,20 +33,6 @@ struct alignas(128) CtlU64 {
 struct alignas(128) CtlI32 {
   int v;
   int pad[31];
-};
-
-struct PoolCtl {
-  CtlU64 buf[3];    // children in buffer (t%2) for state slot s; atomicAdd during an iteration
-  CtlU64 stack[3];  // stack size for state slot s; plain store by workgroup 0
-  CtlU64 tree;      // pushed children (explored tree)
-  CtlU64 sol;       // evaluated leaves (explored solutions)
-  CtlI32 best;      // incumbent (atomicMin by leaves)
-  // plain fields: written by workgroup 0 or by the host between launches
-  u64 bot;          // ring base of the stack
-  u64 parents;      // parents expanded (diagnostics)
-  u64 iters;        // iterations that had work (diagnostics)
-  int overflow;     // set when a ring write would exceed capacity
-  int pad0;
 };
 
 // Workgroup exclusive scan of one int per thread (kBlock threads).

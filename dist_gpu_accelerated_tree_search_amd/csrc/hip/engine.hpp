@@ -21,36 +21,44 @@
 #include <vector>
 
 #include "../core/engine_api.hpp"
-#include "device_common.hpp"
+#include "pool_device.hpp"
 
 namespace tts {
 
 // Traits contract:
-//   using Node; using Args; static constexpr int kMaxChildren(const Args&);
+//   using Node; using Args (with a `PoolArgs<Node> pool` member);
+//   static constexpr int kParentsPerChunk, kChildrenPerChunk, kMaxChunks;
 //   static void launch(const Args&, int t, int grid, hipStream_t);
-//   static int blocks_per_cu();   static int parents_per_block();
+//   static void flatten(const dev::PoolArgs<Node>&, int grid, hipStream_t);
+//   static void finalize(const dev::PoolArgs<Node>&, hipStream_t);
+//   static int blocks_per_cu();
 template <class Traits>
 class DeviceEngine final : public IEngine {
  public:
   using Node = typename Traits::Node;
   using Args = typename Traits::Args;
 
-  DeviceEngine(const EngineConfig& cfg, const Args& problem_args, int max_children) : cfg_(cfg), args_(problem_args) {
+  DeviceEngine(const EngineConfig& cfg, const Args& problem_args) : cfg_(cfg), args_(problem_args) {
     if (cfg_.iters_small % 6 || cfg_.iters_large % 6 || cfg_.iters_small <= 0 || cfg_.iters_large <= 0)
       throw std::invalid_argument("iterations per graph must be positive multiples of 6");
     if (cfg_.max_parents == 0) throw std::invalid_argument("max_parents must be > 0");
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     const auto t0 = std::chrono::steady_clock::now();
-    max_children_ = static_cast<size_t>(max_children);
+    // the parent window is a whole number of chunks, at most kMaxChunks of them
+    const size_t bp = Traits::kParentsPerChunk;
+    max_chunks_ = std::min<size_t>((cfg_.max_parents + bp - 1) / bp, Traits::kMaxChunks);
+    cfg_.max_parents = max_chunks_ * bp;
+    buf_nodes_ = max_chunks_ * static_cast<size_t>(Traits::kChildrenPerChunk);
     size_t cap = 1;
     while (cap * 2 * sizeof(Node) <= cfg_.ring_bytes) cap *= 2;
-    const size_t min_cap = cfg_.max_parents * max_children_ * 8;
-    while (cap < min_cap) cap *= 2;
+    while (cap < buf_nodes_ * 8) cap *= 2;
     cap_ = cap;
-    buf_nodes_ = cfg_.max_parents * max_children_;
     TTS_HIP_CHECK(hipMalloc(&d_ring_, cap_ * sizeof(Node)));
-    TTS_HIP_CHECK(hipMalloc(&d_buf_[0], buf_nodes_ * sizeof(Node)));
-    TTS_HIP_CHECK(hipMalloc(&d_buf_[1], buf_nodes_ * sizeof(Node)));
+    for (int b = 0; b < 2; ++b) {
+      TTS_HIP_CHECK(hipMalloc(&d_buf_[b], buf_nodes_ * sizeof(Node)));
+      TTS_HIP_CHECK(hipMalloc(&d_cnt_[b], max_chunks_ * sizeof(int)));
+      TTS_HIP_CHECK(hipMalloc(&d_lcnt_[b], max_chunks_ * sizeof(int)));
+    }
     TTS_HIP_CHECK(hipMalloc(&d_ctl_, sizeof(dev::PoolCtl)));
     TTS_HIP_CHECK(hipHostMalloc(&h_ctl_, sizeof(dev::PoolCtl), hipHostMallocDefault));
     std::memset(h_ctl_, 0, sizeof(dev::PoolCtl));
@@ -61,20 +69,25 @@ class DeviceEngine final : public IEngine {
       TTS_HIP_CHECK(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking));
       stream_ = own_stream_;
     }
-    args_.stack = d_ring_;
-    args_.buf[0] = d_buf_[0];
-    args_.buf[1] = d_buf_[1];
-    args_.ctl = d_ctl_;
-    args_.cap_mask = cap_ - 1;
-    args_.max_parents = static_cast<int>(cfg_.max_parents);
+    auto& pa = args_.pool;
+    pa.ring = d_ring_;
+    for (int b = 0; b < 2; ++b) {
+      pa.buf[b] = d_buf_[b];
+      pa.cnt[b] = d_cnt_[b];
+      pa.lcnt[b] = d_lcnt_[b];
+    }
+    pa.ctl = d_ctl_;
+    pa.cap_mask = cap_ - 1;
+    pa.max_parents = static_cast<int>(cfg_.max_parents);
+    pa.max_chunks = static_cast<int>(max_chunks_);
     int cus = 0;
     TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+    cus_ = cus;
     const int per_cu = std::max(1, Traits::blocks_per_cu());
-    const size_t want = (cfg_.max_parents + Traits::parents_per_block() - 1) / Traits::parents_per_block();
-    grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(want, static_cast<size_t>(cus) * per_cu)));
+    grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, static_cast<size_t>(cus) * per_cu)));
     upload_ctl();
-    // graphs of 6, 12, 24, ... iterations up to iters_large; run() picks the
-    // largest one whose worst-case ring growth still fits
+    // graphs of 6, 12, 24, ... iterations up to iters_large; run() picks one from
+    // the pool size and the worst-case ring growth
     for (int k = cfg_.iters_small; k <= cfg_.iters_large; k *= 2) {
       ks_.push_back(k);
       if (cfg_.use_graphs) graphs_.push_back(capture(k));
@@ -89,8 +102,11 @@ class DeviceEngine final : public IEngine {
     for (auto g : graphs_) (void)hipGraphExecDestroy(g);
     for (void* p : owned_) (void)hipFree(p);
     (void)hipFree(d_ring_);
-    (void)hipFree(d_buf_[0]);
-    (void)hipFree(d_buf_[1]);
+    for (int b = 0; b < 2; ++b) {
+      (void)hipFree(d_buf_[b]);
+      (void)hipFree(d_cnt_[b]);
+      (void)hipFree(d_lcnt_[b]);
+    }
     (void)hipFree(d_ctl_);
     (void)hipHostFree(h_ctl_);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
@@ -100,6 +116,7 @@ class DeviceEngine final : public IEngine {
   uintptr_t stream() const override { return reinterpret_cast<uintptr_t>(stream_); }
   int device() const override { return cfg_.device; }
   int grid() const { return grid_; }
+  size_t max_parents() const { return cfg_.max_parents; }
   // Device allocations (instance tables) released with the engine.
   void adopt(void* device_ptr) { owned_.push_back(device_ptr); }
 
@@ -191,11 +208,15 @@ class DeviceEngine final : public IEngine {
         upload_ctl();
         total = dev_total();
       }
-      // K iterations can grow the ring by at most K * buf_nodes_: keep headroom.
-      const bool ramp = total < cfg_.max_parents;
+      // Graph size: 6 iterations while ramping up or draining, up to iters_large
+      // when the pool holds many parent windows (fewer host syncs, few idle
+      // trailing iterations); every choice keeps the worst-case ring growth
+      // (K * buf_nodes_) inside the ring.
+      size_t want = 6;
+      while (want < static_cast<size_t>(cfg_.iters_large) && total >= (want / 6) * 2 * cfg_.max_parents) want *= 2;
       int gi = -1;
       for (int i = static_cast<int>(ks_.size()) - 1; i >= 0; --i) {
-        if (ramp && i > 0) continue;
+        if (static_cast<size_t>(ks_[i]) > want && i > 0) continue;
         if (dev_total() + static_cast<size_t>(ks_[i] + 1) * buf_nodes_ <= cap_) {
           gi = i;
           break;
@@ -230,7 +251,8 @@ class DeviceEngine final : public IEngine {
   void reset_counters() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();
-    h_ctl_->tree.v = h_ctl_->sol.v = 0;
+    normalize();
+    h_ctl_->tree = h_ctl_->sol = 0;
     h_ctl_->parents = h_ctl_->iters = 0;
     upload_ctl();
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -239,8 +261,8 @@ class DeviceEngine final : public IEngine {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();
     EngineStats s = stats_;
-    s.tree = h_ctl_->tree.v;
-    s.sol = h_ctl_->sol.v;
+    s.tree = h_ctl_->tree + h_ctl_->pend_children;
+    s.sol = h_ctl_->sol + h_ctl_->pend_leaves;
     s.parents = h_ctl_->parents;
     s.iters = h_ctl_->iters;
     s.best = h_ctl_->best.v;
@@ -256,7 +278,7 @@ class DeviceEngine final : public IEngine {
 
  private:
   size_t dev_stack() const { return static_cast<size_t>(h_ctl_->stack[0].v); }
-  size_t dev_buf() const { return static_cast<size_t>(h_ctl_->buf[0].v); }
+  size_t dev_buf() const { return static_cast<size_t>(h_ctl_->pend_children); }
   size_t dev_total() const { return dev_stack() + dev_buf(); }
 
   void sync_ctl() {
@@ -276,9 +298,21 @@ class DeviceEngine final : public IEngine {
   // which holds between graph replays (K is a multiple of 6).
   void normalize() {
     const size_t c = dev_buf();
-    if (c == 0) return;
-    ring_write_top(d_buf_[0], c, hipMemcpyDeviceToDevice);
-    h_ctl_->buf[0].v = 0;
+    if (c == 0) {
+      h_ctl_->nch[0].v = 0;
+      h_ctl_->sol += h_ctl_->pend_leaves;
+      h_ctl_->pend_leaves = 0;
+      return;
+    }
+    if (dev_stack() + c > cap_) throw std::runtime_error("device ring capacity exceeded");
+    // the flatten kernel reads the device ctl, which equals the host shadow here
+    Traits::flatten(args_.pool, grid_, stream_);
+    TTS_HIP_CHECK(hipGetLastError());
+    h_ctl_->stack[0].v += c;
+    h_ctl_->tree += c;
+    h_ctl_->sol += h_ctl_->pend_leaves;
+    h_ctl_->nch[0].v = 0;
+    h_ctl_->pend_children = h_ctl_->pend_leaves = 0;
   }
 
   void ring_write_top(const Node* src, size_t n, hipMemcpyKind kind) {
@@ -331,6 +365,7 @@ class DeviceEngine final : public IEngine {
       TTS_HIP_CHECK(hipGraphLaunch(graphs_[gi], stream_));
     } else {
       for (int i = 0; i < ks_[gi]; ++i) Traits::launch(args_, i % 6, grid_, stream_);
+      Traits::finalize(args_.pool, stream_);
       TTS_HIP_CHECK(hipGetLastError());
     }
     ++stats_.launches;
@@ -342,6 +377,7 @@ class DeviceEngine final : public IEngine {
     hipGraph_t g;
     TTS_HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     for (int i = 0; i < K; ++i) Traits::launch(args_, i % 6, grid_, cs);
+    Traits::finalize(args_.pool, cs);
     TTS_HIP_CHECK(hipStreamEndCapture(cs, &g));
     hipGraphExec_t exec;
     TTS_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
@@ -352,10 +388,12 @@ class DeviceEngine final : public IEngine {
 
   EngineConfig cfg_;
   Args args_;
-  size_t cap_ = 0, buf_nodes_ = 0, max_children_ = 0;
-  int grid_ = 1;
+  size_t cap_ = 0, buf_nodes_ = 0, max_chunks_ = 0;
+  int grid_ = 1, cus_ = 0;
   Node* d_ring_ = nullptr;
   Node* d_buf_[2] = {nullptr, nullptr};
+  int* d_cnt_[2] = {nullptr, nullptr};
+  int* d_lcnt_[2] = {nullptr, nullptr};
   dev::PoolCtl* d_ctl_ = nullptr;
   dev::PoolCtl* h_ctl_ = nullptr;
   hipStream_t stream_ = nullptr, own_stream_ = nullptr;

@@ -22,8 +22,19 @@ template <int NJ, int M, int LBK>
 struct PfspTraits {
   using Node = PfspNode<NJ>;
   using Args = dev::PfspArgs<NJ, M>;
+  using G = dev::PfspGeom<NJ, LBK>;
+  static constexpr int kParentsPerChunk = G::BP;
+  static constexpr int kChildrenPerChunk = G::MAXCH;
+  static constexpr int kMaxChunks = G::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
+  }
+  static void flatten(const dev::PoolArgs<Node>& pa, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::MAXCH, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
+                       pa);
+  }
+  static void finalize(const dev::PoolArgs<Node>& pa, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, G::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa);
   }
   static int blocks_per_cu() {
     int n = 0;
@@ -32,7 +43,6 @@ struct PfspTraits {
       return 1;
     return n;
   }
-  static int parents_per_block() { return dev::PfspGeom<NJ>::BP; }
 };
 
 // Host-side images of the device tables.
@@ -95,7 +105,7 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   const PfspTableImages img = pfsp_fill_args(in, a);
   a.ptab = upload_vec(img.ptab);
   a.recs = upload_vec(img.recs);
-  auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a, NJ);
+  auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a);
   eng->adopt(const_cast<uint16_t*>(a.ptab));
   eng->adopt(const_cast<uint2*>(a.recs));
   return eng;
@@ -127,7 +137,8 @@ std::vector<int> pfsp_gpu_bounds_t(const PfspInstance& in, const void* parents, 
   a.bounds_out = dbounds;
   a.nparents = static_cast<int>(n);
   a.best_in = best;
-  const int nchunks = static_cast<int>((n + dev::PfspGeom<NJ>::BP - 1) / dev::PfspGeom<NJ>::BP);
+  constexpr int BP = dev::PfspGeom<NJ, LBK>::BP;
+  const int nchunks = static_cast<int>((n + BP - 1) / BP);
   hipLaunchKernelGGL((dev::pfsp_bounds_kernel<NJ, M, LBK>), dim3(std::min(nchunks, 2048)), dim3(dev::kBlock), 0, 0, a);
   TTS_HIP_CHECK(hipGetLastError());
   TTS_HIP_CHECK(hipDeviceSynchronize());

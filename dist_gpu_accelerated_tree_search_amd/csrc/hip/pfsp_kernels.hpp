@@ -17,25 +17,29 @@
 //            scheduled-set bitmask, exiting a lane as soon as lb > best (ref
 //            c_bound_johnson.c:211-237, same pair order => same prune decisions).
 //   Phase C  (expand kernel) prune + stream compaction: one 64-bit ballot per wave
-//            into an LDS bitmap, a popcount scan, ONE device atomic per chunk to
-//            reserve output slots, then each survivor writes its child node
-//            straight into the device-resident pool. Leaves update sol and the
-//            incumbent (atomicMin), exactly the counting rules of
-//            ref PFSP_lib.h:51-95 (generate_children).
+//            into an LDS bitmap, a popcount scan, then each survivor writes its
+//            child node into the chunk's own slot region of the device pool and
+//            the chunk publishes its survivor / leaf counts (pool_device.hpp: no
+//            device atomics). Leaves lower the incumbent (atomicMin), exactly the
+//            counting rules of ref PFSP_lib.h:51-95 (generate_children).
 // Nothing returns to the host per iteration.
 #pragma once
 
 #include <climits>
 
 #include "../core/pfsp_node.hpp"
-#include "device_common.hpp"
+#include "pool_device.hpp"
 
 namespace tts {
 namespace dev {
 
-template <int NJ>
+// Parents per chunk: LB1's per-child cost is O(M) so a chunk holds 256 parents;
+// LB2's is O(M^2 N), so chunks are 8x smaller and spread over 8x more workgroups.
+template <int NJ, int LBK = 1>
 struct PfspGeom {
-  static constexpr int BP = NJ <= 50 ? 256 : (NJ <= 100 ? 128 : (NJ <= 200 ? 64 : 32));  // parents per chunk
+  static constexpr int BP1 = NJ <= 50 ? 256 : (NJ <= 100 ? 128 : (NJ <= 200 ? 64 : 32));
+  static constexpr int BP = LBK == 2 ? (BP1 >= 256 ? 32 : (BP1 / 8 > 8 ? BP1 / 8 : 8)) : BP1;
+  static constexpr int MAXCHUNKS = 2048;
   static constexpr int MAXCH = BP * NJ;                  // children per chunk (upper bound)
   static constexpr int NWORDS = (MAXCH + 63) / 64;       // survivor bitmap words
   static constexpr int NW = (NJ + 63) / 64;              // 64-bit words of a job set
@@ -52,17 +56,13 @@ struct PfspConsts {
 // Kernel arguments (by value -> kernarg segment -> SGPRs for the uniform tables).
 template <int NJ, int M>
 struct PfspArgs {
-  PfspNode<NJ>* stack;     // ring buffer, cap_mask+1 nodes
-  PfspNode<NJ>* buf[2];    // children buffers (ping-pong), max_parents*NJ nodes each
-  PoolCtl* ctl;
+  PoolArgs<PfspNode<NJ>> pool;  // device-resident pool (pool_device.hpp)
   const uint16_t* ptab;    // job-major p, [jobs][MS]
   const uint2* recs;       // LB2 Johnson records, [P][jobs]: {job | p0<<16, p1 | lag<<16}
   const int* offsets;      // bounds kernel only: exclusive prefix of child counts
   int* bounds_out;         // bounds kernel only
   const PfspNode<NJ>* parents_in;  // bounds kernel only
-  u64 cap_mask;
   int jobs;
-  int max_parents;
   int nparents;            // bounds kernel only
   int best_in;             // bounds kernel only
   int min_heads[M];
@@ -74,7 +74,7 @@ struct PfspArgs {
 
 template <int NJ, int M, int LBK>
 struct PfspSmem {
-  using G = PfspGeom<NJ>;
+  using G = PfspGeom<NJ, LBK>;
   using C = PfspConsts<M>;
   static constexpr bool kRecsInLds = (LBK == 2) && (C::P * NJ * 8 <= 32 * 1024);
   PfspNode<NJ> node[G::BP];
@@ -85,10 +85,11 @@ struct PfspSmem {
   u64 bits[G::NWORDS + kBlock / kWave];
   int wpre[kBlock];
   int scan[kBlock / kWave];
-  u64 base;
+  int red[kBlock / kWave];
   u64 pmask[LBK == 2 ? G::BP : 1][G::NW];         // scheduled set (LB2)
   uint16_t cf[LBK == 2 ? kBlock : 1][M];          // child front (LB2)
   uint2 recs[kRecsInLds ? C::P * NJ : 1];
+  PoolSmem<G::MAXCHUNKS> pool;
 };
 
 // ---------------------------------------------------------------------------
@@ -96,7 +97,7 @@ struct PfspSmem {
 // Returns the number of children of the chunk.
 template <int NJ, int M, int LBK, class Src>
 __device__ inline int pfsp_phase_a(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm, int nvalid, Src src) {
-  using G = PfspGeom<NJ>;
+  using G = PfspGeom<NJ, LBK>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
   const int tid = threadIdx.x;
@@ -185,7 +186,7 @@ struct SmemRecs {
 template <int NJ, int M, int LBK>
 __device__ inline int pfsp_child_bound(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm, int c, int best, int& p,
                                        int& k, int& job) {
-  using G = PfspGeom<NJ>;
+  using G = PfspGeom<NJ, LBK>;
   using C = PfspConsts<M>;
   p = sm.map[c];
   const int d = sm.node[p].depth;
@@ -275,63 +276,34 @@ __device__ inline void node_set(uint32_t (&w)[NWD], int e, uint32_t v) {
 }
 
 // ---------------------------------------------------------------------------
-// One B&B iteration on the device-resident pool (see PoolCtl). `t` in [0, 6):
-// state record t%3, children buffer parity t%2.
+// One B&B iteration on the device-resident pool (pool_device.hpp). `t` in [0, 6):
+// state slot t%3, buffer parity t%2.
 template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
-  using G = PfspGeom<NJ>;
+  using G = PfspGeom<NJ, LBK>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
   constexpr int NWD = sizeof(Node) / 4;
   __shared__ PfspSmem<NJ, M, LBK> sm;
   const int tid = threadIdx.x;
-  const int s_in = t % 3, s_out = (t + 1) % 3, s_zero = (t + 2) % 3;
-  Node* const bin = a.buf[t & 1];
-  Node* const bout = a.buf[(t & 1) ^ 1];
-  PoolCtl* ctl = a.ctl;
+  const auto& pa = a.pool;
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
+  if (v.B == 0 || v.overflow) return;
+  const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  Node* const bout = pa.buf[(t & 1) ^ 1];
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
 
-  const u64 S = ctl->stack[s_in].v;
-  const u64 Cn = ctl->buf[s_in].v;
-  const u64 bot = ctl->bot;
-  const u64 B = min(S + Cn, static_cast<u64>(a.max_parents));
-  const u64 nb = min(B, Cn);
-  const u64 ns = B - nb;
-  const u64 L = Cn - nb;  // children of the last iteration not expanded now
-  const u64 Snew = S - ns + L;
-  const bool overflow = Snew > a.cap_mask + 1;
-  const int best = __hip_atomic_load(&ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-  if (blockIdx.x == 0 && tid == 0) {
-    ctl->stack[s_out].v = overflow ? S : Snew;
-    ctl->stack[s_zero].v = 0;
-    ctl->buf[s_zero].v = 0;
-    if (B > 0) {
-      ctl->parents += B;
-      ctl->iters += 1;
-    }
-    if (overflow) ctl->overflow = 1;
-  }
-  if (B == 0 || overflow) return;
-
-  // Leftover children -> top of the ring (disjoint from the parents read below).
-  for (u64 v = static_cast<u64>(blockIdx.x) * kBlock + tid; v < L * VPN; v += static_cast<u64>(gridDim.x) * kBlock) {
-    const u64 i = v / VPN, w = v - i * VPN;
-    const u64 slot = (bot + S + i) & a.cap_mask;
-    reinterpret_cast<uint4*>(a.stack + slot)[w] = reinterpret_cast<const uint4*>(bin + i)[w];
-  }
-
+  pool_spill_leftovers<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, sm.pool);
   pfsp_stage_tables(a, sm);
-  const u64 nchunks = (B + G::BP - 1) / G::BP;
-  u64 my_sol = 0;
-  for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const u64 first = ch * G::BP;
-    const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), B - first));
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+    const u64 first = static_cast<u64>(ch) * G::BP;
+    const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), v.B - first));
     const int total = pfsp_phase_a(a, sm, nvalid, [&](int i) -> const Node* {
-      const u64 gi = first + i;
-      if (gi < nb) return bin + (Cn - nb + gi);
-      return a.stack + ((bot + S - ns + (gi - nb)) & a.cap_mask);
+      return pool_parent<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, first + i, sm.pool);
     });
     // Phase B: bounds, leaves, survivor bitmap.
+    int my_leaves = 0;
     for (int cb = 0; cb < total; cb += kBlock) {
       const int c = cb + tid;
       bool survive = false;
@@ -340,8 +312,8 @@ __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, 
         const int lb = pfsp_child_bound(a, sm, c, best, p, k, job);
         const bool leaf = sm.node[p].depth + 1 == a.jobs;
         if (leaf) {
-          ++my_sol;
-          if (lb < best) atomicMin(&ctl->best.v, lb);
+          ++my_leaves;
+          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
         } else {
           survive = lb < best;
         }
@@ -350,17 +322,18 @@ __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, 
       if ((tid & (kWave - 1)) == 0) sm.bits[c >> 6] = bal;
     }
     __syncthreads();
-    // Phase C: compaction + one atomic slot reservation per chunk.
+    // Phase C: compaction into this chunk's slot region + published counts.
     const int nwords = (total + 63) >> 6;
-    int nsurv = 0;
+    int nsurv = 0, nleaves = 0;
     const int wp = block_exclusive_scan(tid < nwords ? __popcll(sm.bits[tid]) : 0, sm.scan, &nsurv);
+    (void)block_exclusive_scan(my_leaves, sm.red, &nleaves);
     sm.wpre[tid] = wp;
     if (tid == 0) {
-      sm.base = nsurv ? atomicAdd(&ctl->buf[s_out].v, static_cast<u64>(nsurv)) : 0;
-      if (nsurv) atomicAdd(&ctl->tree.v, static_cast<u64>(nsurv));
+      cnt_out[ch] = nsurv;
+      lcnt_out[ch] = nleaves;
     }
     __syncthreads();
-    const u64 base = sm.base;
+    Node* const dst_chunk = bout + static_cast<size_t>(ch) * G::MAXCH;
     for (int c = tid; c < total; c += kBlock) {
       const u64 word = sm.bits[c >> 6];
       if (!((word >> (c & 63)) & 1ull)) continue;
@@ -375,24 +348,19 @@ __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, 
       node_set<NJ>(w, 0, static_cast<uint32_t>(d + 1));
       node_set<NJ>(w, 1 + d, jk);
       node_set<NJ>(w, 1 + k, jd);
-      uint4* dst = reinterpret_cast<uint4*>(bout + base + rank);
+      uint4* dst = reinterpret_cast<uint4*>(dst_chunk + rank);
 #pragma unroll
-      for (int v = 0; v < VPN; ++v) dst[v] = make_uint4(w[4 * v], w[4 * v + 1], w[4 * v + 2], w[4 * v + 3]);
+      for (int q = 0; q < VPN; ++q) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
     }
     __syncthreads();
   }
-  // sol: wave reduction then one atomic per wave
-  u64 s = my_sol;
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
-  if ((tid & (kWave - 1)) == 0 && s) atomicAdd(&ctl->sol.v, s);
 }
 
 // Reference-style evaluation (ref evaluate_gpu, PFSP_gpu_lib.cu:129-152): bounds of
 // every child of `nparents` parents, bounds_out[offsets[i] + (k - depth_i)].
 template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) void pfsp_bounds_kernel(PfspArgs<NJ, M> a) {
-  using G = PfspGeom<NJ>;
+  using G = PfspGeom<NJ, LBK>;
   using Node = PfspNode<NJ>;
   __shared__ PfspSmem<NJ, M, LBK> sm;
   const int tid = threadIdx.x;

@@ -1,0 +1,207 @@
+// Device-resident pool shared by every search kernel — atomic-free.
+//
+// Layout (per GPU):
+//   ring    the stack, ring[(bot + i) & mask] for i < stack size (HBM, 2^k nodes)
+//   bufs    two children buffers (ping-pong). Iteration t expands up to
+//           max_parents parents in chunks of BP; chunk c writes its surviving
+//           children to buf[(t+1)%2][c * MAXCH ...] and their count to cnt[c]
+//           (leaves it evaluated to lcnt[c]). No device atomics: the next
+//           iteration rebuilds the exclusive prefix of cnt[] in LDS (every
+//           workgroup, a few KB of L2 reads) and addresses child i of the
+//           buffer through a binary search of that prefix.
+//   ctl     per-iteration scalars in 3 rotating slots (t%3 read, (t+1)%3
+//           written by workgroup 0), counters, incumbent.
+// Iteration t: parents = the top of [ring ++ buffer] (buffer first: DFS), the
+// buffer's unexpanded part is appended to the ring, children -> other buffer.
+// Nothing goes back to the host per iteration and no two workgroups ever touch
+// the same word, except the incumbent (atomicMin, leaves only).
+//
+// Why not one atomic slot counter per chunk: measured on MI355X, 1024 returning
+// atomicAdds on one word per iteration serialise at ~88/us (~12 us per
+// iteration, profiles/r1_baseline); the prefix costs ~1 us of LDS work.
+#pragma once
+
+#include "device_common.hpp"
+
+namespace tts {
+namespace dev {
+
+struct PoolCtl {
+  CtlU64 stack[3];  // ring occupancy at the start of iteration t (slot t%3)
+  CtlI32 nch[3];    // chunks written by iteration t-1 into buffer t%2
+  // plain counters, updated by workgroup 0 (or the host between launches)
+  u64 tree;         // pushed children (explored tree), lags one iteration
+  u64 sol;          // evaluated leaves (explored solutions), lags one iteration
+  u64 parents;      // parents expanded (diagnostics)
+  u64 iters;        // iterations that had work (diagnostics)
+  u64 bot;          // ring base
+  u64 pend_children;  // children in the latest buffer (finalize kernel)
+  u64 pend_leaves;    // leaves counted by the latest iteration (finalize kernel)
+  int overflow;
+  int pad0;
+  CtlI32 best;      // incumbent (atomicMin by leaves)
+};
+
+template <class Node>
+struct PoolArgs {
+  Node* ring;
+  Node* buf[2];
+  int* cnt[2];
+  int* lcnt[2];
+  PoolCtl* ctl;
+  u64 cap_mask;
+  int max_parents;
+  int max_chunks;
+};
+
+template <int MAXCHUNKS>
+struct PoolSmem {
+  int pre[MAXCHUNKS + 1];
+  int scan[kBlock / kWave];
+  int red[kBlock / kWave];
+};
+
+// Exclusive prefix of cnt[0..n) into pre[0..n] (pre[n] = total) by one workgroup.
+template <int MAXCHUNKS>
+__device__ inline int build_prefix(const int* cnt, int n, PoolSmem<MAXCHUNKS>& ps) {
+  const int per = (n + kBlock - 1) / kBlock;
+  const int lo = min(n, static_cast<int>(threadIdx.x) * per);
+  const int hi = min(n, lo + per);
+  int s = 0;
+  for (int i = lo; i < hi; ++i) s += cnt[i];
+  int total = 0;
+  int run = block_exclusive_scan(s, ps.scan, &total);
+  for (int i = lo; i < hi; ++i) {
+    ps.pre[i] = run;
+    run += cnt[i];
+  }
+  if (threadIdx.x == 0) ps.pre[n] = total;
+  __syncthreads();
+  return total;
+}
+
+// Chunk holding buffered child li: the largest c < n with pre[c] <= li.
+__device__ inline int find_chunk(const int* pre, int n, int li) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pre[mid] <= li)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+struct IterView {
+  u64 S, C, B, nb, ns, L, Snew, bot;
+  int nch_in, nchunks;
+  bool overflow;
+};
+
+// Everything an iteration needs to know, identical in every workgroup; workgroup
+// 0 also publishes the next slot and folds the previous iteration's counts.
+template <class Node, int MAXCHUNKS>
+__device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, PoolSmem<MAXCHUNKS>& ps) {
+  const int s_in = t % 3, s_out = (t + 1) % 3;
+  const int b_in = t & 1;
+  PoolCtl* ctl = pa.ctl;
+  IterView v;
+  v.S = ctl->stack[s_in].v;
+  v.nch_in = ctl->nch[s_in].v;
+  v.bot = ctl->bot;
+  v.C = static_cast<u64>(build_prefix(pa.cnt[b_in], v.nch_in, ps));
+  v.B = min(v.S + v.C, static_cast<u64>(pa.max_parents));
+  v.nb = min(v.B, v.C);
+  v.ns = v.B - v.nb;
+  v.L = v.C - v.nb;
+  v.Snew = v.S - v.ns + v.L;
+  v.overflow = v.Snew > pa.cap_mask + 1;
+  v.nchunks = static_cast<int>((v.B + BP - 1) / BP);
+  if (blockIdx.x == 0) {
+    // leaves evaluated by the previous iteration
+    int lf = 0;
+    for (int i = threadIdx.x; i < v.nch_in; i += kBlock) lf += pa.lcnt[b_in][i];
+    int lf_total = 0;
+    (void)block_exclusive_scan(lf, ps.red, &lf_total);
+    if (threadIdx.x == 0) {
+      ctl->stack[s_out].v = v.overflow ? v.S : v.Snew;
+      ctl->nch[s_out].v = v.overflow ? 0 : v.nchunks;
+      ctl->tree += v.C;
+      ctl->sol += static_cast<u64>(lf_total);
+      if (v.B > 0) {
+        ctl->parents += v.B;
+        ctl->iters += 1;
+      }
+      if (v.overflow) ctl->overflow = 1;
+    }
+  }
+  return v;
+}
+
+// Address of logical element i of the pool window read by this iteration:
+// buffer children first (top of the DFS stack), then the ring top.
+template <class Node, int MAXCH, int MAXCHUNKS>
+__device__ inline const Node* pool_parent(const PoolArgs<Node>& pa, const IterView& v, int t, u64 gi,
+                                          const PoolSmem<MAXCHUNKS>& ps) {
+  if (gi < v.nb) {
+    const int li = static_cast<int>(v.C - v.nb + gi);
+    const int c = find_chunk(ps.pre, v.nch_in, li);
+    return pa.buf[t & 1] + static_cast<size_t>(c) * MAXCH + (li - ps.pre[c]);
+  }
+  return pa.ring + ((v.bot + v.S - v.ns + (gi - v.nb)) & pa.cap_mask);
+}
+
+// Buffered children not expanded this iteration go to the ring top.
+template <class Node, int MAXCH, int MAXCHUNKS>
+__device__ inline void pool_spill_leftovers(const PoolArgs<Node>& pa, const IterView& v, int t,
+                                            const PoolSmem<MAXCHUNKS>& ps) {
+  constexpr int VPN = sizeof(Node) / 16;
+  const Node* bin = pa.buf[t & 1];
+  for (u64 x = static_cast<u64>(blockIdx.x) * kBlock + threadIdx.x; x < v.L * VPN;
+       x += static_cast<u64>(gridDim.x) * kBlock) {
+    const int li = static_cast<int>(x / VPN);
+    const int w = static_cast<int>(x - static_cast<u64>(li) * VPN);
+    const int c = find_chunk(ps.pre, v.nch_in, li);
+    const Node* src = bin + static_cast<size_t>(c) * MAXCH + (li - ps.pre[c]);
+    Node* dst = pa.ring + ((v.bot + v.S + li) & pa.cap_mask);
+    reinterpret_cast<uint4*>(dst)[w] = reinterpret_cast<const uint4*>(src)[w];
+  }
+}
+
+// Host-requested: move the whole buffer (slot 0 / buffer 0, i.e. between graph
+// replays) onto the ring top. The host then folds the counts into ctl.
+template <class Node, int MAXCH, int MAXCHUNKS>
+__global__ __launch_bounds__(kBlock) void pool_flatten_kernel(PoolArgs<Node> pa) {
+  __shared__ PoolSmem<MAXCHUNKS> ps;
+  IterView v;
+  v.S = pa.ctl->stack[0].v;
+  v.bot = pa.ctl->bot;
+  v.nch_in = pa.ctl->nch[0].v;
+  v.C = static_cast<u64>(build_prefix(pa.cnt[0], v.nch_in, ps));
+  v.nb = 0;
+  v.L = v.C;
+  pool_spill_leftovers<Node, MAXCH, MAXCHUNKS>(pa, v, 0, ps);
+}
+
+// Last node of every graph: counts of the latest buffer for the host.
+template <class Node, int MAXCHUNKS>
+__global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa) {
+  __shared__ PoolSmem<MAXCHUNKS> ps;
+  const int n = pa.ctl->nch[0].v;
+  int c = 0, l = 0;
+  for (int i = threadIdx.x; i < n; i += kBlock) {
+    c += pa.cnt[0][i];
+    l += pa.lcnt[0][i];
+  }
+  int ct = 0, lt = 0;
+  (void)block_exclusive_scan(c, ps.scan, &ct);
+  (void)block_exclusive_scan(l, ps.red, &lt);
+  if (threadIdx.x == 0) {
+    pa.ctl->pend_children = static_cast<u64>(ct);
+    pa.ctl->pend_leaves = static_cast<u64>(lt);
+  }
+}
+
+}  // namespace dev
+}  // namespace tts

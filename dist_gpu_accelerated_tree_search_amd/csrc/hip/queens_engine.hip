@@ -7,8 +7,19 @@ namespace tts {
 struct QueensTraits {
   using Node = QueensNode;
   using Args = dev::QueensArgs;
+  using S = dev::QueensSmem;
+  static constexpr int kParentsPerChunk = S::BP;
+  static constexpr int kChildrenPerChunk = S::MAXCH;
+  static constexpr int kMaxChunks = S::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL(dev::queens_expand_kernel, dim3(grid), dim3(dev::kBlock), 0, s, a, t);
+  }
+  static void flatten(const dev::PoolArgs<Node>& pa, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, S::MAXCH, S::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
+                       pa);
+  }
+  static void finalize(const dev::PoolArgs<Node>& pa, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, S::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa);
   }
   static int blocks_per_cu() {
     int n = 0;
@@ -16,7 +27,6 @@ struct QueensTraits {
       return 1;
     return n;
   }
-  static int parents_per_block() { return dev::QueensSmem::BP; }
 };
 
 static dev::QueensArgs queens_args(int N, int G) {
@@ -31,7 +41,7 @@ static dev::QueensArgs queens_args(int N, int G) {
 
 std::unique_ptr<IEngine> make_queens_engine(int N, int G, const EngineConfig& cfg) {
   TTS_HIP_CHECK(hipSetDevice(cfg.device));
-  return std::make_unique<DeviceEngine<QueensTraits>>(cfg, queens_args(N, G), N);
+  return std::make_unique<DeviceEngine<QueensTraits>>(cfg, queens_args(N, G));
 }
 
 std::vector<uint8_t> queens_gpu_labels(int N, int G, const QueensNode* parents, size_t n, int device) {

@@ -12,24 +12,20 @@
 //            child->parent map in LDS, leaves (depth == N) counted as solutions.
 //   Phase B  thread-per-child: the r-th free row of its parent via a 5-step popcount
 //            search, then consecutive threads store consecutive 16-B children:
-//            fully coalesced writes into the device pool after ONE device atomic
-//            per chunk reserved the slots.
+//            fully coalesced writes into the chunk's slot region of the device
+//            pool (pool_device.hpp, no device atomics).
 #pragma once
 
 #include "../core/pfsp_node.hpp"
-#include "device_common.hpp"
+#include "pool_device.hpp"
 
 namespace tts {
 namespace dev {
 
 struct QueensArgs {
-  QueensNode* stack;
-  QueensNode* buf[2];
-  PoolCtl* ctl;
-  u64 cap_mask;
+  PoolArgs<QueensNode> pool;
   int N;
   int G;
-  int max_parents;
   uint32_t full;
   // labels kernel only (reference-style evaluation, tests)
   const QueensNode* parents_in;
@@ -40,12 +36,14 @@ struct QueensArgs {
 struct QueensSmem {
   static constexpr int BP = kBlock;
   static constexpr int MAXCH = BP * 32;
+  static constexpr int MAXCHUNKS = 4096;
   QueensNode node[BP];
   uint32_t avail[BP];
   int off[BP];
   uint8_t map[MAXCH];
   int scan[kBlock / kWave];
-  u64 base;
+  int red[kBlock / kWave];
+  PoolSmem<MAXCHUNKS> pool;
 };
 
 __device__ inline uint32_t queens_free_rows(const QueensNode& nd, uint32_t full, int G) {
@@ -74,75 +72,50 @@ __device__ inline int nth_set_bit(uint32_t x, int r) {
 }
 
 __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int t) {
+  using S = QueensSmem;
   __shared__ QueensSmem sm;
   const int tid = threadIdx.x;
-  const int s_in = t % 3, s_out = (t + 1) % 3, s_zero = (t + 2) % 3;
-  QueensNode* const bin = a.buf[t & 1];
-  QueensNode* const bout = a.buf[(t & 1) ^ 1];
-  PoolCtl* ctl = a.ctl;
+  const auto& pa = a.pool;
+  const IterView v = pool_begin<QueensNode, S::MAXCHUNKS>(pa, t, S::BP, sm.pool);
+  if (v.B == 0 || v.overflow) return;
+  QueensNode* const bout = pa.buf[(t & 1) ^ 1];
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  pool_spill_leftovers<QueensNode, S::MAXCH, S::MAXCHUNKS>(pa, v, t, sm.pool);
 
-  const u64 S = ctl->stack[s_in].v;
-  const u64 Cn = ctl->buf[s_in].v;
-  const u64 bot = ctl->bot;
-  const u64 B = min(S + Cn, static_cast<u64>(a.max_parents));
-  const u64 nb = min(B, Cn);
-  const u64 ns = B - nb;
-  const u64 L = Cn - nb;
-  const u64 Snew = S - ns + L;
-  const bool overflow = Snew > a.cap_mask + 1;
-  if (blockIdx.x == 0 && tid == 0) {
-    ctl->stack[s_out].v = overflow ? S : Snew;
-    ctl->stack[s_zero].v = 0;
-    ctl->buf[s_zero].v = 0;
-    if (B > 0) {
-      ctl->parents += B;
-      ctl->iters += 1;
-    }
-    if (overflow) ctl->overflow = 1;
-  }
-  if (B == 0 || overflow) return;
-
-  for (u64 i = static_cast<u64>(blockIdx.x) * kBlock + tid; i < L; i += static_cast<u64>(gridDim.x) * kBlock)
-    a.stack[(bot + S + i) & a.cap_mask] = bin[i];
-
-  const u64 nchunks = (B + QueensSmem::BP - 1) / QueensSmem::BP;
-  u64 my_sol = 0;
-  for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const u64 gi = ch * QueensSmem::BP + tid;
-    int nchild = 0;
-    if (gi < B) {
-      const QueensNode nd = gi < nb ? bin[Cn - nb + gi] : a.stack[(bot + S - ns + (gi - nb)) & a.cap_mask];
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+    const u64 gi = static_cast<u64>(ch) * S::BP + tid;
+    int nchild = 0, leaf = 0;
+    if (gi < v.B) {
+      const QueensNode nd = *pool_parent<QueensNode, S::MAXCH, S::MAXCHUNKS>(pa, v, t, gi, sm.pool);
       sm.node[tid] = nd;
       if (static_cast<int>(nd.depth) == a.N) {
-        ++my_sol;
+        leaf = 1;
       } else {
         const uint32_t av = queens_free_rows(nd, a.full, a.G);
         sm.avail[tid] = av;
         nchild = __popc(av);
       }
     }
-    int total = 0;
+    int total = 0, leaves = 0;
     const int off = block_exclusive_scan(nchild, sm.scan, &total);
+    (void)block_exclusive_scan(leaf, sm.red, &leaves);
     sm.off[tid] = off;
     for (int j = 0; j < nchild; ++j) sm.map[off + j] = static_cast<uint8_t>(tid);
     if (tid == 0) {
-      sm.base = total ? atomicAdd(&ctl->buf[s_out].v, static_cast<u64>(total)) : 0;
-      if (total) atomicAdd(&ctl->tree.v, static_cast<u64>(total));
+      cnt_out[ch] = total;
+      lcnt_out[ch] = leaves;
     }
     __syncthreads();
-    const u64 base = sm.base;
+    QueensNode* const dst = bout + static_cast<size_t>(ch) * S::MAXCH;
     for (int c = tid; c < total; c += kBlock) {
       const int p = sm.map[c];
       const QueensNode nd = sm.node[p];
       const uint32_t bit = 1u << nth_set_bit(sm.avail[p], c - sm.off[p]);
-      bout[base + c] = QueensNode{nd.cols | bit, (nd.diag | bit) << 1, (nd.anti | bit) >> 1, nd.depth + 1};
+      dst[c] = QueensNode{nd.cols | bit, (nd.diag | bit) << 1, (nd.anti | bit) >> 1, nd.depth + 1};
     }
     __syncthreads();
   }
-  u64 s = my_sol;
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
-  if ((tid & (kWave - 1)) == 0 && s) atomicAdd(&ctl->sol.v, s);
 }
 
 // Reference-style labels (ref evaluate_gpu): labels[i*N + k] = 1 iff row k is a
