@@ -61,6 +61,10 @@ class DeviceEngine final : public IEngine {
     }
     TTS_HIP_CHECK(hipMalloc(&d_ctl_, sizeof(dev::PoolCtl)));
     TTS_HIP_CHECK(hipHostMalloc(&h_ctl_, sizeof(dev::PoolCtl), hipHostMallocDefault));
+    TTS_HIP_CHECK(hipHostMalloc(&h_up_, sizeof(dev::PoolCtl), hipHostMallocDefault));
+    TTS_HIP_CHECK(hipHostMalloc(&h_mirror_, sizeof(dev::PoolCtl), hipHostMallocMapped | hipHostMallocCoherent));
+    TTS_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_mirror_), h_mirror_, 0));
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&up_done_, hipEventDisableTiming));
     std::memset(h_ctl_, 0, sizeof(dev::PoolCtl));
     h_ctl_->best.v = 0x7fffffff;
     if (cfg_.external_stream) {
@@ -77,6 +81,7 @@ class DeviceEngine final : public IEngine {
       pa.lcnt[b] = d_lcnt_[b];
     }
     pa.ctl = d_ctl_;
+    pa.mirror = d_mirror_;
     pa.cap_mask = cap_ - 1;
     pa.max_parents = static_cast<int>(cfg_.max_parents);
     pa.max_chunks = static_cast<int>(max_chunks_);
@@ -109,6 +114,9 @@ class DeviceEngine final : public IEngine {
     }
     (void)hipFree(d_ctl_);
     (void)hipHostFree(h_ctl_);
+    (void)hipHostFree(h_up_);
+    (void)hipHostFree(h_mirror_);
+    (void)hipEventDestroy(up_done_);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
   }
 
@@ -241,7 +249,6 @@ class DeviceEngine final : public IEngine {
     sync_ctl();
     h_ctl_->best.v = b;
     upload_ctl();
-    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
   }
   int best() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
@@ -255,7 +262,6 @@ class DeviceEngine final : public IEngine {
     h_ctl_->tree = h_ctl_->sol = 0;
     h_ctl_->parents = h_ctl_->iters = 0;
     upload_ctl();
-    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
   }
   EngineStats stats() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
@@ -281,17 +287,26 @@ class DeviceEngine final : public IEngine {
   size_t dev_buf() const { return static_cast<size_t>(h_ctl_->pend_children); }
   size_t dev_total() const { return dev_stack() + dev_buf(); }
 
+  // Bring the host shadow up to date. After a graph replay the finalize kernel has
+  // already published the control block to host-mapped memory: one stream
+  // synchronisation, no copy. Otherwise the shadow is current by construction
+  // (every host edit is uploaded from it).
   void sync_ctl() {
+    if (!mirror_pending_) return;
     const auto t0 = std::chrono::steady_clock::now();
-    TTS_HIP_CHECK(hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(dev::PoolCtl), hipMemcpyDeviceToHost, stream_));
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    std::memcpy(h_ctl_, h_mirror_, sizeof(dev::PoolCtl));
+    mirror_pending_ = false;
     ++stats_.syncs;
     stats_.t_memcpy += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
+  // Asynchronous upload of the host shadow (through its own pinned staging copy,
+  // so the shadow can be edited again immediately).
   void upload_ctl() {
-    TTS_HIP_CHECK(hipMemcpyAsync(d_ctl_, h_ctl_, sizeof(dev::PoolCtl), hipMemcpyHostToDevice, stream_));
-    // pinned source: make sure the copy consumed it before the host edits it again
-    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    TTS_HIP_CHECK(hipEventSynchronize(up_done_));
+    std::memcpy(h_up_, h_ctl_, sizeof(dev::PoolCtl));
+    TTS_HIP_CHECK(hipMemcpyAsync(d_ctl_, h_up_, sizeof(dev::PoolCtl), hipMemcpyHostToDevice, stream_));
+    TTS_HIP_CHECK(hipEventRecord(up_done_, stream_));
   }
 
   // Host shadow must be current (sync_ctl) and state slot 0 / buffer 0 active,
@@ -361,6 +376,7 @@ class DeviceEngine final : public IEngine {
   }
 
   void launch_iters(int gi) {
+    mirror_pending_ = true;
     if (cfg_.use_graphs) {
       TTS_HIP_CHECK(hipGraphLaunch(graphs_[gi], stream_));
     } else {
@@ -396,6 +412,11 @@ class DeviceEngine final : public IEngine {
   int* d_lcnt_[2] = {nullptr, nullptr};
   dev::PoolCtl* d_ctl_ = nullptr;
   dev::PoolCtl* h_ctl_ = nullptr;
+  dev::PoolCtl* h_up_ = nullptr;
+  dev::PoolCtl* h_mirror_ = nullptr;
+  dev::PoolCtl* d_mirror_ = nullptr;
+  hipEvent_t up_done_ = nullptr;
+  bool mirror_pending_ = false;
   hipStream_t stream_ = nullptr, own_stream_ = nullptr;
   std::vector<int> ks_;
   std::vector<hipGraphExec_t> graphs_;

@@ -276,10 +276,86 @@ __device__ inline void node_set(uint32_t (&w)[NWD], int e, uint32_t v) {
 }
 
 // ---------------------------------------------------------------------------
+// LB1 / LB1_d: thread-per-parent. The parent's front and remain live in registers
+// (M is a template constant, loops fully unrolled); each child costs O(M) with
+// one vectorised LDS read of its job's p row — no child->parent map, no per-child
+// gathers of parent rows, no bitmap. The i-th child's bound is handed to `emit`.
+template <int NJ, int M>
+struct PfspSmemLB1 {
+  using G = PfspGeom<NJ, 1>;
+  using C = PfspConsts<M>;
+  PfspNode<NJ> node[G::BP];
+  uint16_t ptab[NJ][C::MS];
+  int scan[kBlock / kWave];
+  int red[kBlock / kWave];
+  PoolSmem<G::MAXCHUNKS> pool;
+};
+
+template <int M>
+__device__ inline void load_prow(const uint16_t* row, int (&pr)[M]) {
+  constexpr int MS = PfspConsts<M>::MS;
+  const uint4* r4 = reinterpret_cast<const uint4*>(row);
+#pragma unroll
+  for (int q = 0; q < MS / 8; ++q) {
+    const uint4 x = r4[q];
+    const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+      if (q * 8 + h < M) pr[q * 8 + h] = static_cast<int>((wv[h >> 1] >> ((h & 1) * 16)) & 0xffffu);
+  }
+}
+
+template <int NJ, int M, class Smem, class Emit>
+__device__ inline void pfsp_lb1_parent(const PfspArgs<NJ, M>& a, Smem& sm, int p, Emit emit) {
+  const PfspNode<NJ>& nd = sm.node[p];
+  const int d = nd.depth;
+  int f[M], r[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    f[m] = (d == 0) ? a.min_heads[m] : 0;
+    r[m] = a.sum_all[m];
+  }
+  for (int i = 0; i < d; ++i) {
+    int pr[M];
+    load_prow<M>(sm.ptab[nd.prmu[i]], pr);
+    f[0] += pr[0];
+    r[0] -= pr[0];
+#pragma unroll
+    for (int m = 1; m < M; ++m) {
+      f[m] = max(f[m - 1], f[m]) + pr[m];
+      r[m] -= pr[m];
+    }
+  }
+  for (int k = d; k < a.jobs; ++k) {
+    const int job = nd.prmu[k];
+    int pr[M];
+    load_prow<M>(sm.ptab[job], pr);
+    // child front on machine m = s + p[m]; parent remain still holds p[m][job]:
+    // max over m of (child front + child remain + min tail)  (ref c_bound_simple.c:219-244)
+    int lb = f[0] + r[0] + a.min_tails[0];
+    int t = f[0] + pr[0];
+#pragma unroll
+    for (int m = 1; m < M; ++m) {
+      const int s = max(t, f[m]);
+      lb = max(lb, s + r[m] + a.min_tails[m]);
+      t = s + pr[m];
+    }
+    emit(k - d, k, lb);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // One B&B iteration on the device-resident pool (pool_device.hpp). `t` in [0, 6):
 // state slot t%3, buffer parity t%2.
+template <int NJ, int M>
+__device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
+
 template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
+  if constexpr (LBK != 2) {
+    pfsp_expand_lb1<NJ, M>(a, t);
+    return;
+  }
   using G = PfspGeom<NJ, LBK>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
@@ -356,26 +432,140 @@ __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, 
   }
 }
 
+// LB1 / LB1_d expand: per chunk, thread p owns parent p end to end.
+template <int NJ, int M>
+__device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
+  using G = PfspGeom<NJ, 1>;
+  using Node = PfspNode<NJ>;
+  using id_t = typename Node::id_t;
+  constexpr int VPN = sizeof(Node) / 16;
+  constexpr int NWD = sizeof(Node) / 4;
+  constexpr int SW = (NJ + 63) / 64;  // survivor mask words
+  __shared__ PfspSmemLB1<NJ, M> sm;
+  const int tid = threadIdx.x;
+  const auto& pa = a.pool;
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
+  if (v.B == 0 || v.overflow) return;
+  const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  Node* const bout = pa.buf[(t & 1) ^ 1];
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  pool_spill_leftovers<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, sm.pool);
+  {
+    constexpr int MS = PfspConsts<M>::MS;
+    uint16_t* pt = &sm.ptab[0][0];
+    for (int i = tid; i < a.jobs * MS; i += kBlock) pt[i] = a.ptab[i];
+  }
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+    const u64 first = static_cast<u64>(ch) * G::BP;
+    const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), v.B - first));
+    for (int x = tid; x < nvalid * VPN; x += kBlock) {
+      const int i = x / VPN, w = x - i * VPN;
+      reinterpret_cast<uint4*>(&sm.node[i])[w] =
+          reinterpret_cast<const uint4*>(pool_parent<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, first + i, sm.pool))[w];
+    }
+    __syncthreads();
+    u64 surv[SW];
+#pragma unroll
+    for (int q = 0; q < SW; ++q) surv[q] = 0;
+    int nsurv = 0, nleaf = 0;
+    if (tid < nvalid) {
+      const bool leaf = sm.node[tid].depth + 1 == a.jobs;
+      pfsp_lb1_parent<NJ, M>(a, sm, tid, [&](int j, int /*k*/, int lb) {
+        if (leaf) {
+          ++nleaf;
+          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+        } else if (lb < best) {
+          ++nsurv;
+#pragma unroll
+          for (int q = 0; q < SW; ++q)
+            if ((j >> 6) == q) surv[q] |= 1ull << (j & 63);
+        }
+      });
+    }
+    int total = 0, leaves = 0;
+    const int off = block_exclusive_scan(nsurv, sm.scan, &total);
+    (void)block_exclusive_scan(nleaf, sm.red, &leaves);
+    if (tid == 0) {
+      cnt_out[ch] = total;
+      lcnt_out[ch] = leaves;
+    }
+    if (nsurv) {
+      const Node& nd = sm.node[tid];
+      const int d = nd.depth;
+      uint32_t w[NWD];
+#pragma unroll
+      for (int i = 0; i < NWD; ++i) w[i] = reinterpret_cast<const uint32_t*>(&nd)[i];
+      const uint32_t jd = nd.prmu[d];
+      node_set<NJ>(w, 0, static_cast<uint32_t>(d + 1));
+      Node* dst = bout + static_cast<size_t>(ch) * G::MAXCH + off;
+#pragma unroll
+      for (int q = 0; q < SW; ++q) {
+        u64 m = surv[q];
+        while (m) {
+          const int j = q * 64 + __ffsll(static_cast<long long>(m)) - 1;
+          m &= m - 1;
+          const int k = d + j;
+          uint32_t c[NWD];
+#pragma unroll
+          for (int i = 0; i < NWD; ++i) c[i] = w[i];
+          node_set<NJ>(c, 1 + d, static_cast<uint32_t>(nd.prmu[k]));
+          node_set<NJ>(c, 1 + k, jd);
+          uint4* o = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+          for (int qq = 0; qq < VPN; ++qq) o[qq] = make_uint4(c[4 * qq], c[4 * qq + 1], c[4 * qq + 2], c[4 * qq + 3]);
+          ++dst;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  (void)sizeof(id_t);
+}
+
 // Reference-style evaluation (ref evaluate_gpu, PFSP_gpu_lib.cu:129-152): bounds of
 // every child of `nparents` parents, bounds_out[offsets[i] + (k - depth_i)].
 template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) void pfsp_bounds_kernel(PfspArgs<NJ, M> a) {
   using G = PfspGeom<NJ, LBK>;
   using Node = PfspNode<NJ>;
-  __shared__ PfspSmem<NJ, M, LBK> sm;
   const int tid = threadIdx.x;
-  pfsp_stage_tables(a, sm);
-  const int nchunks = (a.nparents + G::BP - 1) / G::BP;
-  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const int first = ch * G::BP;
-    const int nvalid = min(G::BP, a.nparents - first);
-    const int total = pfsp_phase_a(a, sm, nvalid, [&](int i) -> const Node* { return a.parents_in + first + i; });
-    for (int c = tid; c < total; c += kBlock) {
-      int p, k, job;
-      const int lb = pfsp_child_bound(a, sm, c, a.best_in, p, k, job);
-      a.bounds_out[a.offsets[first + p] + (k - sm.node[p].depth)] = lb;
+  if constexpr (LBK != 2) {
+    constexpr int VPN = sizeof(Node) / 16;
+    __shared__ PfspSmemLB1<NJ, M> sm;
+    constexpr int MS = PfspConsts<M>::MS;
+    uint16_t* pt = &sm.ptab[0][0];
+    for (int i = tid; i < a.jobs * MS; i += kBlock) pt[i] = a.ptab[i];
+    const int nchunks = (a.nparents + G::BP - 1) / G::BP;
+    for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+      const int first = ch * G::BP;
+      const int nvalid = min(G::BP, a.nparents - first);
+      __syncthreads();
+      for (int x = tid; x < nvalid * VPN; x += kBlock) {
+        const int i = x / VPN, w = x - i * VPN;
+        reinterpret_cast<uint4*>(&sm.node[i])[w] = reinterpret_cast<const uint4*>(a.parents_in + first + i)[w];
+      }
+      __syncthreads();
+      if (tid < nvalid) {
+        int* out = a.bounds_out + a.offsets[first + tid];
+        pfsp_lb1_parent<NJ, M>(a, sm, tid, [&](int j, int, int lb) { out[j] = lb; });
+      }
     }
-    __syncthreads();
+  } else {
+    __shared__ PfspSmem<NJ, M, LBK> sm;
+    pfsp_stage_tables(a, sm);
+    const int nchunks = (a.nparents + G::BP - 1) / G::BP;
+    for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+      const int first = ch * G::BP;
+      const int nvalid = min(G::BP, a.nparents - first);
+      const int total = pfsp_phase_a(a, sm, nvalid, [&](int i) -> const Node* { return a.parents_in + first + i; });
+      for (int c = tid; c < total; c += kBlock) {
+        int p, k, job;
+        const int lb = pfsp_child_bound(a, sm, c, a.best_in, p, k, job);
+        a.bounds_out[a.offsets[first + p] + (k - sm.node[p].depth)] = lb;
+      }
+      __syncthreads();
+    }
   }
 }
 

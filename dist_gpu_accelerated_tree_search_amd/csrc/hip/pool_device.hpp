@@ -21,6 +21,8 @@
 // iteration, profiles/r1_baseline); the prefix costs ~1 us of LDS work.
 #pragma once
 
+#include <cstddef>
+
 #include "device_common.hpp"
 
 namespace tts {
@@ -49,6 +51,7 @@ struct PoolArgs {
   int* cnt[2];
   int* lcnt[2];
   PoolCtl* ctl;
+  PoolCtl* mirror;  // host-mapped pinned copy written by the finalize kernel
   u64 cap_mask;
   int max_parents;
   int max_chunks;
@@ -200,6 +203,20 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   if (threadIdx.x == 0) {
     pa.ctl->pend_children = static_cast<u64>(ct);
     pa.ctl->pend_leaves = static_cast<u64>(lt);
+  }
+  __syncthreads();
+  // publish the whole control block to host-mapped memory: the host reads it
+  // after the graph completes, without a device-to-host copy
+  static_assert(sizeof(PoolCtl) % 4 == 0, "ctl must be dword-sized");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(pa.ctl);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(pa.mirror);
+  for (int i = threadIdx.x; i < static_cast<int>(sizeof(PoolCtl) / 4); i += kBlock) {
+    uint32_t x = src[i];
+    if (i == static_cast<int>(offsetof(PoolCtl, pend_children) / 4)) x = static_cast<uint32_t>(ct);
+    if (i == static_cast<int>(offsetof(PoolCtl, pend_children) / 4) + 1) x = 0;
+    if (i == static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4)) x = static_cast<uint32_t>(lt);
+    if (i == static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4) + 1) x = 0;
+    __hip_atomic_store(dst + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
