@@ -22,7 +22,7 @@ template <int NJ, int M, int LBK>
 struct PfspTraits {
   using Node = PfspNode<NJ>;
   using Args = dev::PfspArgs<NJ, M>;
-  using G = dev::PfspGeom<NJ, LBK>;
+  using G = dev::PfspGeom<NJ, LBK, M>;
   static constexpr int kParentsPerChunk = G::BP;
   static constexpr int kChildrenPerChunk = G::MAXCH;
   static constexpr int kMaxChunks = G::MAXCHUNKS;
@@ -137,7 +137,7 @@ std::vector<int> pfsp_gpu_bounds_t(const PfspInstance& in, const void* parents, 
   a.bounds_out = dbounds;
   a.nparents = static_cast<int>(n);
   a.best_in = best;
-  constexpr int BP = dev::PfspGeom<NJ, LBK>::BP;
+  constexpr int BP = dev::PfspGeom<NJ, LBK, M>::BP;
   const int nchunks = static_cast<int>((n + BP - 1) / BP);
   hipLaunchKernelGGL((dev::pfsp_bounds_kernel<NJ, M, LBK>), dim3(std::min(nchunks, 2048)), dim3(dev::kBlock), 0, 0, a);
   TTS_HIP_CHECK(hipGetLastError());

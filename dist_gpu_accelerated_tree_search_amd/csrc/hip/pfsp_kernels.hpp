@@ -34,12 +34,14 @@ namespace tts {
 namespace dev {
 
 // Parents per chunk: LB1's per-child cost is O(M) so a chunk holds 256 parents;
-// LB2's is O(M^2 N), so chunks are 8x smaller and spread over 8x more workgroups.
-template <int NJ, int LBK = 1>
+// LB2's is O(M^2 N / 2): chunks shrink with the number of machine pairs so an
+// iteration spreads over as many workgroups as the chip holds.
+template <int NJ, int LBK = 1, int M = 20>
 struct PfspGeom {
   static constexpr int BP1 = NJ <= 50 ? 256 : (NJ <= 100 ? 128 : (NJ <= 200 ? 64 : 32));
-  static constexpr int BP = LBK == 2 ? (BP1 >= 256 ? 32 : (BP1 / 8 > 8 ? BP1 / 8 : 8)) : BP1;
-  static constexpr int MAXCHUNKS = 2048;
+  static constexpr int BP2 = M <= 5 ? BP1 : (M <= 10 ? BP1 / 4 : BP1 / 8);
+  static constexpr int BP = LBK == 2 ? (BP2 > 8 ? BP2 : 8) : BP1;
+  static constexpr int MAXCHUNKS = LBK == 2 ? 4096 : 2048;
   static constexpr int MAXCH = BP * NJ;                  // children per chunk (upper bound)
   static constexpr int NWORDS = (MAXCH + 63) / 64;       // survivor bitmap words
   static constexpr int NW = (NJ + 63) / 64;              // 64-bit words of a job set
@@ -74,7 +76,7 @@ struct PfspArgs {
 
 template <int NJ, int M, int LBK>
 struct PfspSmem {
-  using G = PfspGeom<NJ, LBK>;
+  using G = PfspGeom<NJ, LBK, M>;
   using C = PfspConsts<M>;
   static constexpr bool kRecsInLds = (LBK == 2) && (C::P * NJ * 8 <= 32 * 1024);
   PfspNode<NJ> node[G::BP];
@@ -97,7 +99,7 @@ struct PfspSmem {
 // Returns the number of children of the chunk.
 template <int NJ, int M, int LBK, class Src>
 __device__ inline int pfsp_phase_a(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm, int nvalid, Src src) {
-  using G = PfspGeom<NJ, LBK>;
+  using G = PfspGeom<NJ, LBK, M>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
   const int tid = threadIdx.x;
@@ -186,7 +188,7 @@ struct SmemRecs {
 template <int NJ, int M, int LBK>
 __device__ inline int pfsp_child_bound(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm, int c, int best, int& p,
                                        int& k, int& job) {
-  using G = PfspGeom<NJ, LBK>;
+  using G = PfspGeom<NJ, LBK, M>;
   using C = PfspConsts<M>;
   p = sm.map[c];
   const int d = sm.node[p].depth;
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, 
     pfsp_expand_lb1<NJ, M>(a, t);
     return;
   }
-  using G = PfspGeom<NJ, LBK>;
+  using G = PfspGeom<NJ, LBK, M>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
   constexpr int NWD = sizeof(Node) / 4;
@@ -527,7 +529,7 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
 // every child of `nparents` parents, bounds_out[offsets[i] + (k - depth_i)].
 template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) void pfsp_bounds_kernel(PfspArgs<NJ, M> a) {
-  using G = PfspGeom<NJ, LBK>;
+  using G = PfspGeom<NJ, LBK, M>;
   using Node = PfspNode<NJ>;
   const int tid = threadIdx.x;
   if constexpr (LBK != 2) {
