@@ -70,6 +70,19 @@ inline void bind_engine(py::module_& m) {
       .def("size", &IEngine::size, py::call_guard<py::gil_scoped_release>())
       .def("run", &IEngine::run, py::arg("max_launches") = -1, py::arg("max_seconds") = 0.0,
            py::arg("stop_below") = 0, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "solve",
+          [](IEngine& e, U8 a, int best) {
+            if (a.ndim() != 2 || static_cast<size_t>(a.shape(1)) != e.node_bytes())
+              throw std::invalid_argument("nodes must be a (n, node_bytes) uint8 array");
+            EngineStats st;
+            {
+              py::gil_scoped_release nogil;
+              st = e.solve_from(a.data(), static_cast<size_t>(a.shape(0)), best);
+            }
+            return engine_stats_dict(st);
+          },
+          py::arg("nodes"), py::arg("best"), "Complete solve from these nodes (counters reset); returns stats.")
       .def_property("best", &IEngine::best, &IEngine::set_best)
       .def("reset_counters", &IEngine::reset_counters)
       .def("stats", [](IEngine& e) { return engine_stats_dict(e.stats()); })

@@ -71,6 +71,14 @@ class CpuEngine final : public IEngine {
     return launches;
   }
 
+  EngineStats solve_from(const void* nodes, size_t n, int best) override {
+    reset_counters();
+    best_ = best;
+    push_host(nodes, n);
+    run(-1, 0.0, 0);
+    return stats();
+  }
+
   EngineStats stats() override {
     EngineStats s;
     s.tree = tree_;

@@ -62,8 +62,12 @@ class DeviceEngine final : public IEngine {
     TTS_HIP_CHECK(hipMalloc(&d_ctl_, sizeof(dev::PoolCtl)));
     TTS_HIP_CHECK(hipHostMalloc(&h_ctl_, sizeof(dev::PoolCtl), hipHostMallocDefault));
     TTS_HIP_CHECK(hipHostMalloc(&h_up_, sizeof(dev::PoolCtl), hipHostMallocDefault));
-    TTS_HIP_CHECK(hipHostMalloc(&h_mirror_, sizeof(dev::PoolCtl), hipHostMallocMapped | hipHostMallocCoherent));
-    TTS_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_mirror_), h_mirror_, 0));
+    for (int m = 0; m < 2; ++m) {
+      TTS_HIP_CHECK(
+          hipHostMalloc(&h_mirror_[m], sizeof(dev::PoolCtl), hipHostMallocMapped | hipHostMallocCoherent));
+      TTS_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_mirror_[m]), h_mirror_[m], 0));
+      TTS_HIP_CHECK(hipEventCreateWithFlags(&graph_done_[m], hipEventDisableTiming));
+    }
     TTS_HIP_CHECK(hipEventCreateWithFlags(&up_done_, hipEventDisableTiming));
     std::memset(h_ctl_, 0, sizeof(dev::PoolCtl));
     h_ctl_->best.v = 0x7fffffff;
@@ -81,7 +85,7 @@ class DeviceEngine final : public IEngine {
       pa.lcnt[b] = d_lcnt_[b];
     }
     pa.ctl = d_ctl_;
-    pa.mirror = d_mirror_;
+    pa.mirror = d_mirror_[0];
     pa.cap_mask = cap_ - 1;
     pa.max_parents = static_cast<int>(cfg_.max_parents);
     pa.max_chunks = static_cast<int>(max_chunks_);
@@ -95,7 +99,8 @@ class DeviceEngine final : public IEngine {
     // the pool size and the worst-case ring growth
     for (int k = cfg_.iters_small; k <= cfg_.iters_large; k *= 2) {
       ks_.push_back(k);
-      if (cfg_.use_graphs) graphs_.push_back(capture(k));
+      if (cfg_.use_graphs)
+        for (int m = 0; m < 2; ++m) graphs_[m].push_back(capture(k, m));
     }
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
     stats_.t_malloc = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -104,7 +109,8 @@ class DeviceEngine final : public IEngine {
   ~DeviceEngine() override {
     (void)hipSetDevice(cfg_.device);
     if (stream_) (void)hipStreamSynchronize(stream_);
-    for (auto g : graphs_) (void)hipGraphExecDestroy(g);
+    for (auto& gs : graphs_)
+      for (auto g : gs) (void)hipGraphExecDestroy(g);
     for (void* p : owned_) (void)hipFree(p);
     (void)hipFree(d_ring_);
     for (int b = 0; b < 2; ++b) {
@@ -115,7 +121,10 @@ class DeviceEngine final : public IEngine {
     (void)hipFree(d_ctl_);
     (void)hipHostFree(h_ctl_);
     (void)hipHostFree(h_up_);
-    (void)hipHostFree(h_mirror_);
+    for (int m = 0; m < 2; ++m) {
+      (void)hipHostFree(h_mirror_[m]);
+      (void)hipEventDestroy(graph_done_[m]);
+    }
     (void)hipEventDestroy(up_done_);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
   }
@@ -198,50 +207,81 @@ class DeviceEngine final : public IEngine {
   long run(long max_launches, double max_seconds, size_t stop_below) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     const auto t0 = std::chrono::steady_clock::now();
+    auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
     long launches = 0;
     sync_ctl();
     for (;;) {
+      // ---- nothing in flight: the host shadow is the device state ----
       if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
       size_t total = dev_total();
       if (total + spill_.size() == 0) break;
       if (total + spill_.size() < stop_below) break;
       if (max_launches >= 0 && launches >= max_launches) break;
-      if (max_seconds > 0 &&
-          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >= max_seconds)
-        break;
-      // refill from the host spill when the device runs low
-      if (total < cfg_.max_parents && !spill_.empty()) {
+      if (max_seconds > 0 && elapsed() >= max_seconds) break;
+      if (total < cfg_.max_parents && !spill_.empty()) {  // refill from the host spill
         normalize();
         refill(cfg_.max_parents * 4);
         upload_ctl();
         total = dev_total();
       }
-      // Graph size: 6 iterations while ramping up or draining, up to iters_large
-      // when the pool holds many parent windows (fewer host syncs, few idle
-      // trailing iterations); every choice keeps the worst-case ring growth
-      // (K * buf_nodes_) inside the ring.
-      size_t want = 6;
-      while (want < static_cast<size_t>(cfg_.iters_large) && total >= (want / 6) * 2 * cfg_.max_parents) want *= 2;
-      int gi = -1;
-      for (int i = static_cast<int>(ks_.size()) - 1; i >= 0; --i) {
-        if (static_cast<size_t>(ks_[i]) > want && i > 0) continue;
-        if (dev_total() + static_cast<size_t>(ks_[i] + 1) * buf_nodes_ <= cap_) {
-          gi = i;
-          break;
-        }
-      }
+      int gi = pick_graph(total, 0);
       if (gi < 0) {
         normalize();
         spill_bottom(dev_stack() / 2 + 1);
         upload_ctl();
         continue;
       }
-      launch_iters(gi);
+      launch_graph(gi);
       ++launches;
-      sync_ctl();
+      // ---- pipelined replays: while one graph runs, queue the next one if the
+      // last known pool spans at least one parent window and the worst-case
+      // growth of both fits; then read the older graph's mirror. Hides the host
+      // sync + launch gap between replays. ----
+      size_t known = total;
+      size_t inflight_growth = static_cast<size_t>(ks_[gi] + 1) * buf_nodes_;
+      while (!inflight_.empty()) {
+        const bool budget_ok = (max_launches < 0 || launches < max_launches) && (max_seconds <= 0 || elapsed() < max_seconds);
+        if (inflight_.size() == 1 && budget_ok && known >= cfg_.max_parents) {
+          const int g2 = pick_graph(known, inflight_growth);
+          if (g2 >= 0) {
+            launch_graph(g2);
+            ++launches;
+            inflight_growth += static_cast<size_t>(ks_[g2] + 1) * buf_nodes_;
+          }
+        }
+        wait_oldest();
+        if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
+        known = dev_total();
+        inflight_growth = inflight_.empty() ? 0 : static_cast<size_t>(ks_[inflight_k_.front()] + 1) * buf_nodes_;
+      }
     }
-    stats_.t_run += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    stats_.t_run += elapsed();
     return launches;
+  }
+
+  // Fused start of a complete solve: fresh counters and incumbent, `n` root-level
+  // nodes loaded at the ring base, one control upload, run to exhaustion.
+  EngineStats solve_from(const void* nodes, size_t n, int best) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    normalize();
+    if (dev_total() != 0 || !spill_.empty() || n > cap_ / 2) {
+      reset_counters();
+      set_best(best);
+      push_host(nodes, n);
+    } else {
+      h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
+      h_ctl_->best.v = best;
+      h_ctl_->bot = 0;
+      h_ctl_->stack[0].v = 0;
+      h_ctl_->nch[0].v = 0;
+      h_ctl_->pend_children = h_ctl_->pend_leaves = 0;
+      h_ctl_->overflow = 0;
+      ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
+      upload_ctl();
+    }
+    run(-1, 0.0, 0);
+    return stats();
   }
 
   void set_best(int b) override {
@@ -292,13 +332,29 @@ class DeviceEngine final : public IEngine {
   // synchronisation, no copy. Otherwise the shadow is current by construction
   // (every host edit is uploaded from it).
   void sync_ctl() {
-    if (!mirror_pending_) return;
+    while (!inflight_.empty()) wait_oldest();
+  }
+  void wait_oldest() {
     const auto t0 = std::chrono::steady_clock::now();
-    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
-    std::memcpy(h_ctl_, h_mirror_, sizeof(dev::PoolCtl));
-    mirror_pending_ = false;
+    const int m = inflight_.front();
+    inflight_.pop_front();
+    inflight_k_.pop_front();
+    TTS_HIP_CHECK(hipEventSynchronize(graph_done_[m]));
+    std::memcpy(h_ctl_, h_mirror_[m], sizeof(dev::PoolCtl));
     ++stats_.syncs;
     stats_.t_memcpy += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  // Largest graph whose worst-case ring growth (plus `extra` already in flight)
+  // fits, no longer than the pool size suggests: 6 iterations while ramping up or
+  // draining, more when the pool holds several parent windows.
+  int pick_graph(size_t total, size_t extra) const {
+    size_t want = 6;
+    while (want < static_cast<size_t>(cfg_.iters_large) && total >= (want / 6) * 2 * cfg_.max_parents) want *= 2;
+    for (int i = static_cast<int>(ks_.size()) - 1; i >= 0; --i) {
+      if (static_cast<size_t>(ks_[i]) > want && i > 0) continue;
+      if (total + extra + static_cast<size_t>(ks_[i] + 1) * buf_nodes_ <= cap_) return i;
+    }
+    return -1;
   }
   // Asynchronous upload of the host shadow (through its own pinned staging copy,
   // so the shadow can be edited again immediately).
@@ -375,25 +431,33 @@ class DeviceEngine final : public IEngine {
     stats_.refilled += m;
   }
 
-  void launch_iters(int gi) {
-    mirror_pending_ = true;
+  void launch_graph(int gi) {
+    const int m = next_mirror_;
+    next_mirror_ ^= 1;
     if (cfg_.use_graphs) {
-      TTS_HIP_CHECK(hipGraphLaunch(graphs_[gi], stream_));
+      TTS_HIP_CHECK(hipGraphLaunch(graphs_[m][gi], stream_));
     } else {
       for (int i = 0; i < ks_[gi]; ++i) Traits::launch(args_, i % 6, grid_, stream_);
-      Traits::finalize(args_.pool, stream_);
+      auto pa = args_.pool;
+      pa.mirror = d_mirror_[m];
+      Traits::finalize(pa, stream_);
       TTS_HIP_CHECK(hipGetLastError());
     }
+    TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
+    inflight_.push_back(m);
+    inflight_k_.push_back(gi);
     ++stats_.launches;
   }
 
-  hipGraphExec_t capture(int K) {
+  hipGraphExec_t capture(int K, int mirror) {
     hipStream_t cs;
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     hipGraph_t g;
     TTS_HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     for (int i = 0; i < K; ++i) Traits::launch(args_, i % 6, grid_, cs);
-    Traits::finalize(args_.pool, cs);
+    auto pa = args_.pool;
+    pa.mirror = d_mirror_[mirror];
+    Traits::finalize(pa, cs);
     TTS_HIP_CHECK(hipStreamEndCapture(cs, &g));
     hipGraphExec_t exec;
     TTS_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
@@ -413,13 +477,15 @@ class DeviceEngine final : public IEngine {
   dev::PoolCtl* d_ctl_ = nullptr;
   dev::PoolCtl* h_ctl_ = nullptr;
   dev::PoolCtl* h_up_ = nullptr;
-  dev::PoolCtl* h_mirror_ = nullptr;
-  dev::PoolCtl* d_mirror_ = nullptr;
+  dev::PoolCtl* h_mirror_[2] = {nullptr, nullptr};
+  dev::PoolCtl* d_mirror_[2] = {nullptr, nullptr};
+  hipEvent_t graph_done_[2] = {nullptr, nullptr};
   hipEvent_t up_done_ = nullptr;
-  bool mirror_pending_ = false;
+  int next_mirror_ = 0;
+  std::deque<int> inflight_, inflight_k_;
   hipStream_t stream_ = nullptr, own_stream_ = nullptr;
   std::vector<int> ks_;
-  std::vector<hipGraphExec_t> graphs_;
+  std::vector<hipGraphExec_t> graphs_[2];
   std::vector<void*> owned_;
   std::vector<Node> spill_;
   EngineStats stats_;

@@ -66,11 +66,8 @@ def solve_engine(model, engine, ub: int = 1, m: int = 25, best: int | None = Non
     if verbose:
         from .utils.report import phase
         print(phase("Initial search on CPU completed", tree1, sol1, t1 - t0))
-    engine.reset_counters()
-    engine.best = int(best)
-    engine.push(nodes)
-    launches = engine.run()
-    st = engine.stats()
+    st = engine.solve(nodes, int(best))  # reset + load + run to exhaustion, one native call
+    launches = st["launches"]
     best = min(best, st["best"])
     t2 = time.perf_counter()
     tree, sol = tree1 + st["tree"], sol1 + st["sol"]
