@@ -83,6 +83,14 @@ inline void bind_engine(py::module_& m) {
             return engine_stats_dict(st);
           },
           py::arg("nodes"), py::arg("best"), "Complete solve from these nodes (counters reset); returns stats.")
+      .def(
+          "begin",
+          [](IEngine& e, U8 a, int best) {
+            if (a.ndim() != 2 || static_cast<size_t>(a.shape(1)) != e.node_bytes())
+              throw std::invalid_argument("nodes must be a (n, node_bytes) uint8 array");
+            e.begin(a.data(), static_cast<size_t>(a.shape(0)), best);
+          },
+          py::arg("nodes"), py::arg("best"), "Fresh start from these nodes (counters reset), without running.")
       .def_property("best", &IEngine::best, &IEngine::set_best)
       .def("reset_counters", &IEngine::reset_counters)
       .def("stats", [](IEngine& e) { return engine_stats_dict(e.stats()); })

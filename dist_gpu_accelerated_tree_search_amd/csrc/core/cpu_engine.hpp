@@ -71,10 +71,14 @@ class CpuEngine final : public IEngine {
     return launches;
   }
 
-  EngineStats solve_from(const void* nodes, size_t n, int best) override {
+  void begin(const void* nodes, size_t n, int best) override {
     reset_counters();
+    pool_.clear();
     best_ = best;
     push_host(nodes, n);
+  }
+  EngineStats solve_from(const void* nodes, size_t n, int best) override {
+    begin(nodes, n, best);
     run(-1, 0.0, 0);
     return stats();
   }

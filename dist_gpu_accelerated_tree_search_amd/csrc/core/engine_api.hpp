@@ -40,7 +40,9 @@ class IEngine {
   // launched (<0: unlimited), `max_seconds` elapsed (<=0: unlimited), or the pool
   // dropped below `stop_below` nodes. Returns the number of graph launches.
   virtual long run(long max_launches, double max_seconds, size_t stop_below) = 0;
-  // One complete solve from `n` nodes with incumbent `best` (counters reset).
+  // Fresh start (counters reset, incumbent set) from `n` nodes, without running.
+  virtual void begin(const void* nodes, size_t n, int best) = 0;
+  // One complete solve from `n` nodes with incumbent `best` (begin + run + stats).
   virtual EngineStats solve_from(const void* nodes, size_t n, int best) = 0;
   virtual void set_best(int b) = 0;
   virtual int best() = 0;

@@ -259,9 +259,9 @@ class DeviceEngine final : public IEngine {
     return launches;
   }
 
-  // Fused start of a complete solve: fresh counters and incumbent, `n` root-level
-  // nodes loaded at the ring base, one control upload, run to exhaustion.
-  EngineStats solve_from(const void* nodes, size_t n, int best) override {
+  // Fused start of a solve: fresh counters and incumbent, `n` nodes loaded at the
+  // ring base, one asynchronous control upload (no stream synchronisation).
+  void begin(const void* nodes, size_t n, int best) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();
     normalize();
@@ -269,17 +269,21 @@ class DeviceEngine final : public IEngine {
       reset_counters();
       set_best(best);
       push_host(nodes, n);
-    } else {
-      h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
-      h_ctl_->best.v = best;
-      h_ctl_->bot = 0;
-      h_ctl_->stack[0].v = 0;
-      h_ctl_->nch[0].v = 0;
-      h_ctl_->pend_children = h_ctl_->pend_leaves = 0;
-      h_ctl_->overflow = 0;
-      ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
-      upload_ctl();
+      return;
     }
+    h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
+    h_ctl_->best.v = best;
+    h_ctl_->bot = 0;
+    h_ctl_->stack[0].v = 0;
+    h_ctl_->nch[0].v = 0;
+    h_ctl_->pend_children = h_ctl_->pend_leaves = 0;
+    h_ctl_->overflow = 0;
+    ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
+    upload_ctl();
+  }
+
+  EngineStats solve_from(const void* nodes, size_t n, int best) override {
+    begin(nodes, n, best);
     run(-1, 0.0, 0);
     return stats();
   }

@@ -80,14 +80,22 @@ class PfspModel:
     def root(self) -> np.ndarray:
         return nodes_mod.pfsp_root(self.jobs)
 
+    @property
+    def host_lb(self) -> int:
+        """Bound used by host-side steps: LB1 is evaluated with the incremental LB1_d
+        (identical values), as the reference's CPU workers do
+        (ref pfsp_multigpu_cuda.c:152-154: `if (lb == 1) cpulb = 0`)."""
+        return 0 if self.lb == 1 else self.lb
+
     def warmup(self, best: int, target: int):
         """Step 1 (ref pfsp_multigpu_cuda.c:111-118): breadth-first on the host until
         `target` nodes. Returns (nodes, tree, sol, best)."""
-        return ops.cpu().pfsp_bfs(self.native, self.lb, int(best), int(target))
+        return ops.cpu().pfsp_bfs(self.native, self.host_lb, int(best), int(target))
 
     def drain(self, best: int, nodes: np.ndarray):
         """Step 3 (ref :488-495): depth-first over leftovers. Returns (tree, sol, best)."""
-        return ops.cpu().pfsp_drain(self.native, self.lb, int(best), np.ascontiguousarray(nodes, dtype=np.uint8))
+        return ops.cpu().pfsp_drain(self.native, self.host_lb, int(best),
+                                    np.ascontiguousarray(nodes, dtype=np.uint8))
 
     # ---- engines ----
     def make_engine(self, backend: str = "gpu", device: int = 0, opts: EngineOptions | None = None):

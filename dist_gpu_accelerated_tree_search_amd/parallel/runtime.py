@@ -78,12 +78,18 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
     # ---- Step 1: redundant, deterministic host warm-up on every rank ----
     best = model.initial_best(ub)
     nodes, tree1, sol1, best = model.warmup(best, world * cfg.init_per_rank)
-    mine = nodes[round_robin_share(len(nodes), rank, world)]
-    engine.reset_counters()
-    engine.best = int(best)
-    if len(mine):
-        engine.push(np.ascontiguousarray(mine))
+    mine = np.ascontiguousarray(nodes[round_robin_share(len(nodes), rank, world)])
     rs.t_init = time.perf_counter() - t_start
+    if world == 1:  # one fused native solve, no rounds
+        st = engine.solve(mine, int(best))
+        elapsed = time.perf_counter() - t_start
+        w = WorkerStats(tree=int(st["tree"]), sol=int(st["sol"]), gen_child=int(st["tree"]),
+                        t_memcpy=float(st["t_memcpy"]), t_malloc=float(st["t_malloc"]), t_kernel=float(st["t_run"]))
+        return SolveResult(best=min(int(best), int(st["best"])), tree=tree1 + int(st["tree"]),
+                           sol=sol1 + int(st["sol"]), elapsed=elapsed, t_init=rs.t_init,
+                           t_search=elapsed - rs.t_init, workers=[w],
+                           extra={"rounds": 0, "sent_nodes": [0], "received_nodes": [0], "world": 1})
+    engine.begin(mine, int(best))
 
     # ---- Step 2: rounds ----
     share = cfg.ws or cfg.L
