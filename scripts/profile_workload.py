@@ -1,0 +1,21 @@
+"""Fixed workloads for rocprofv3 runs (kernel trace / PMC counters)."""
+import sys
+sys.path.insert(0, ".")
+import torch  # noqa: F401
+from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel, QueensModel, solve_engine
+
+which = sys.argv[1] if len(sys.argv) > 1 else "ta014"
+if which == "ta014":
+    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=4 << 30))
+    for _ in range(20):
+        r = solve_engine(m, eng)
+elif which == "ta008":
+    m = PfspModel(8, 0); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30))
+    r = solve_engine(m, eng)
+elif which == "lb2":
+    m = PfspModel(20, 2); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30))
+    r = solve_engine(m, eng)
+elif which == "queens":
+    m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30))
+    r = solve_engine(m, eng)
+print(which, r.tree, r.sol, r.best, f"{r.elapsed*1e3:.2f} ms")
