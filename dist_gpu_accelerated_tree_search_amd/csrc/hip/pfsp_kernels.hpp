@@ -52,7 +52,11 @@ struct PfspGeom {
 template <int M>
 struct PfspConsts {
   static constexpr int P = M * (M - 1) / 2;
-  static constexpr int MS = (M + 7) & ~7;  // u16 row stride of the LDS p table (16-B rows)
+  // u16 row stride of the LDS p table: 16 B for M <= 8, else 48 B. A 48-B stride
+  // (12 dwords) sends the 16 rows a ds_read_b128 lane group touches to 16
+  // different bank quads; a 32-B stride would put rows j and j+8 on the same banks.
+  static constexpr int MS = M <= 8 ? 8 : ((M + 7) & ~7) == 16 ? 24 : ((M + 7) & ~7);
+  static constexpr int RV = (M + 7) / 8;   // 16-B vectors holding one row's M values
 };
 
 // Kernel arguments (by value -> kernarg segment -> SGPRs for the uniform tables).
@@ -295,10 +299,9 @@ struct PfspSmemLB1 {
 
 template <int M>
 __device__ inline void load_prow(const uint16_t* row, int (&pr)[M]) {
-  constexpr int MS = PfspConsts<M>::MS;
   const uint4* r4 = reinterpret_cast<const uint4*>(row);
 #pragma unroll
-  for (int q = 0; q < MS / 8; ++q) {
+  for (int q = 0; q < PfspConsts<M>::RV; ++q) {
     const uint4 x = r4[q];
     const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -351,11 +354,16 @@ __device__ inline void pfsp_lb1_parent(const PfspArgs<NJ, M>& a, Smem& sm, int p
 // state slot t%3, buffer parity t%2.
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
+template <int NJ, int M>
+__device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 
 template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK != 2) {
-    pfsp_expand_lb1<NJ, M>(a, t);
+    if constexpr (sizeof(PfspNode<NJ>) == 32)
+      pfsp_expand_lb1_small<NJ, M>(a, t);
+    else
+      pfsp_expand_lb1<NJ, M>(a, t);
     return;
   }
   using G = PfspGeom<NJ, LBK, M>;
@@ -431,6 +439,154 @@ __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, 
       for (int q = 0; q < VPN; ++q) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
     }
     __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 20-job bucket (NJ <= 32, 32-B nodes): the parent node lives in 8 registers. The
+// prefix and children loops are unrolled over all NJ positions and predicated on
+// the depth, so every job id is extracted with a static shift (v_bfe) — no LDS
+// node reads at all (the previous LDS node rows were read byte-wise by 64 lanes
+// with a 32-B stride: 8-way bank conflicts, profiles/r1_pmc). The only LDS
+// traffic is one padded p-table row per scheduled job and per child.
+template <int NJ>
+__device__ inline uint32_t node_byte(const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], int e) {
+  constexpr int NWD = sizeof(PfspNode<NJ>) / 4;
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < NWD; ++i) x = (i == (e >> 2)) ? w[i] : x;
+  return (x >> ((e & 3) * 8)) & 0xffu;
+}
+
+template <int NJ, int M>
+struct PfspSmemLB1s {
+  using G = PfspGeom<NJ, 1>;
+  uint16_t ptab[NJ][PfspConsts<M>::MS];
+  int scan[kBlock / kWave];
+  PoolSmem<G::MAXCHUNKS> pool;
+};
+
+// Bounds of every child of the parent held in w (valid lanes only); calls
+// emit(k, lb) for each child position k (static after unrolling).
+template <int NJ, int M, class Emit>
+__device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const uint16_t (*ptab)[PfspConsts<M>::MS],
+                                        const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], Emit emit) {
+  const int d = static_cast<int>(w[0] & 0xffu);
+  int f[M], r[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    f[m] = (d == 0) ? a.min_heads[m] : 0;
+    r[m] = a.sum_all[m];
+  }
+#pragma unroll
+  for (int i = 0; i < NJ - 1; ++i) {
+    if (i < d) {
+      const int job = static_cast<int>((w[(1 + i) >> 2] >> (((1 + i) & 3) * 8)) & 0xffu);
+      int pr[M];
+      load_prow<M>(ptab[job], pr);
+      f[0] += pr[0];
+      r[0] -= pr[0];
+#pragma unroll
+      for (int m = 1; m < M; ++m) {
+        f[m] = max(f[m - 1], f[m]) + pr[m];
+        r[m] -= pr[m];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    if (k >= d && k < a.jobs) {
+      const int job = static_cast<int>((w[(1 + k) >> 2] >> (((1 + k) & 3) * 8)) & 0xffu);
+      int pr[M];
+      load_prow<M>(ptab[job], pr);
+      int lb = f[0] + r[0] + a.min_tails[0];
+      int tt = f[0] + pr[0];
+#pragma unroll
+      for (int m = 1; m < M; ++m) {
+        const int sv = max(tt, f[m]);
+        lb = max(lb, sv + r[m] + a.min_tails[m]);
+        tt = sv + pr[m];
+      }
+      emit(k, lb);
+    }
+  }
+}
+
+template <int NJ, int M>
+__device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
+  using G = PfspGeom<NJ, 1>;
+  using Node = PfspNode<NJ>;
+  constexpr int NWD = sizeof(Node) / 4;
+  static_assert(NJ <= 32 && sizeof(Node) == 32, "register path is for the 20-job bucket");
+  __shared__ PfspSmemLB1s<NJ, M> sm;
+  const int tid = threadIdx.x;
+  const auto& pa = a.pool;
+  {  // p table -> LDS (made visible by pool_begin's barriers)
+    uint16_t* pt = &sm.ptab[0][0];
+    for (int i = tid; i < a.jobs * PfspConsts<M>::MS; i += kBlock) pt[i] = a.ptab[i];
+  }
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
+  if (v.B == 0 || v.overflow) return;
+  const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  Node* const bout = pa.buf[(t & 1) ^ 1];
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  pool_spill_leftovers<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, sm.pool);
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+    const u64 gi = static_cast<u64>(ch) * G::BP + tid;
+    const bool valid = gi < v.B;
+    uint32_t w[NWD];
+    if (valid) {
+      const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, gi, sm.pool));
+      const uint4 x0 = src[0], x1 = src[1];
+      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < NWD; ++i) w[i] = 0;
+    }
+    const int d = static_cast<int>(w[0] & 0xffu);
+    const bool leaf = d + 1 == a.jobs;
+    uint32_t surv = 0;
+    int nsurv = 0, nleaf = 0;
+    if (valid) {
+      lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+        if (leaf) {
+          ++nleaf;
+          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+        } else if (lb < best) {
+          ++nsurv;
+          surv |= 1u << k;
+        }
+      });
+    }
+    // one scan for both counts: survivors in the low 16 bits, leaves in the high
+    int tot = 0;
+    const int off = block_exclusive_scan(nsurv | (nleaf << 16), sm.scan, &tot) & 0xffff;
+    if (tid == 0) {
+      cnt_out[ch] = tot & 0xffff;
+      lcnt_out[ch] = tot >> 16;
+    }
+    if (surv) {
+      const uint32_t jd = node_byte<NJ>(w, 1 + d);
+      uint32_t base[NWD];
+#pragma unroll
+      for (int i = 0; i < NWD; ++i) base[i] = w[i];
+      base[0] = (base[0] & ~0xffu) | static_cast<uint32_t>(d + 1);
+      uint4* dst = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::MAXCH + off);
+      while (surv) {
+        const int k = __ffs(surv) - 1;
+        surv &= surv - 1;
+        uint32_t c[NWD];
+#pragma unroll
+        for (int i = 0; i < NWD; ++i) c[i] = base[i];
+        node_set<NJ>(c, 1 + d, node_byte<NJ>(w, 1 + k));
+        node_set<NJ>(c, 1 + k, jd);
+        dst[0] = make_uint4(c[0], c[1], c[2], c[3]);
+        dst[1] = make_uint4(c[4], c[5], c[6], c[7]);
+        dst += 2;
+      }
+    }
   }
 }
 
@@ -532,7 +688,23 @@ __global__ __launch_bounds__(kBlock) void pfsp_bounds_kernel(PfspArgs<NJ, M> a) 
   using G = PfspGeom<NJ, LBK, M>;
   using Node = PfspNode<NJ>;
   const int tid = threadIdx.x;
-  if constexpr (LBK != 2) {
+  if constexpr (LBK != 2 && sizeof(Node) == 32) {
+    __shared__ PfspSmemLB1s<NJ, M> sm;
+    constexpr int MS = PfspConsts<M>::MS;
+    uint16_t* pt = &sm.ptab[0][0];
+    for (int i = tid; i < a.jobs * MS; i += kBlock) pt[i] = a.ptab[i];
+    __syncthreads();
+    for (int i = blockIdx.x * kBlock + tid; i < a.nparents; i += gridDim.x * kBlock) {
+      uint32_t w[8];
+      const uint4* src = reinterpret_cast<const uint4*>(a.parents_in + i);
+      const uint4 x0 = src[0], x1 = src[1];
+      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+      const int d = static_cast<int>(w[0] & 0xffu);
+      int* out = a.bounds_out + a.offsets[i];
+      lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) { out[k - d] = lb; });
+    }
+  } else if constexpr (LBK != 2) {
     constexpr int VPN = sizeof(Node) / 16;
     __shared__ PfspSmemLB1<NJ, M> sm;
     constexpr int MS = PfspConsts<M>::MS;
