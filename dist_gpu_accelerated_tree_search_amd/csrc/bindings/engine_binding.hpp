@@ -10,6 +10,7 @@
 #include <stdexcept>
 
 #include "../core/engine_api.hpp"
+#include "../core/runner.hpp"
 
 namespace py = pybind11;
 
@@ -95,6 +96,58 @@ inline void bind_engine(py::module_& m) {
       .def("reset_counters", &IEngine::reset_counters)
       .def("stats", [](IEngine& e) { return engine_stats_dict(e.stats()); })
       .def("synchronize", &IEngine::synchronize, py::call_guard<py::gil_scoped_release>());
+}
+
+// run_workers(engines, initial_nodes, best, ...) -> {"best": int, "workers": [dict]}
+inline void bind_runner(py::module_& m) {
+  using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+  m.def(
+      "run_workers",
+      [](py::list engines, py::list initial, int best, size_t m_, size_t steal_cap, double slice_min, double slice_max,
+         bool ws) {
+        if (engines.size() != initial.size()) throw std::invalid_argument("one initial node array per engine");
+        std::vector<IEngine*> es;
+        std::vector<std::vector<uint8_t>> init;
+        for (size_t i = 0; i < engines.size(); ++i) {
+          IEngine* e = engines[i].cast<IEngine*>();
+          U8 a = initial[i].cast<U8>();
+          if (a.ndim() != 2 || static_cast<size_t>(a.shape(1)) != e->node_bytes())
+            throw std::invalid_argument("initial nodes must be (n, node_bytes) uint8 arrays");
+          es.push_back(e);
+          init.emplace_back(a.data(), a.data() + a.size());
+        }
+        RunnerConfig cfg;
+        cfg.m = m_;
+        cfg.steal_cap = steal_cap;
+        cfg.slice_min = slice_min;
+        cfg.slice_max = slice_max;
+        cfg.work_sharing = ws;
+        std::vector<WorkerReport> rep;
+        {
+          py::gil_scoped_release nogil;
+          rep = run_workers(es, init, best, cfg);
+        }
+        py::list ws_out;
+        for (auto& r : rep) {
+          py::dict d = engine_stats_dict(r.st);
+          d["rounds"] = r.rounds;
+          d["sent"] = r.sent;
+          d["received"] = r.received;
+          d["transfers_in"] = r.transfers_in;
+          d["transfers_out"] = r.transfers_out;
+          d["t_run_w"] = r.t_run;
+          d["t_comm"] = r.t_comm;
+          d["t_idle"] = r.t_idle;
+          ws_out.append(d);
+        }
+        py::dict out;
+        out["best"] = best;
+        out["workers"] = ws_out;
+        return out;
+      },
+      py::arg("engines"), py::arg("initial"), py::arg("best"), py::arg("m") = 25, py::arg("steal_cap") = 250000,
+      py::arg("slice_min") = 0.0005, py::arg("slice_max") = 0.05, py::arg("ws") = true,
+      "Drive several engines (GPUs and/or CPU workers) from one process until all pools are empty.");
 }
 
 }  // namespace tts

@@ -78,6 +78,7 @@ MulticoreConfig mc_config(size_t m, size_t batch, size_t steal_cap, bool ws) {
 PYBIND11_MODULE(_tts_cpu, m) {
   m.doc() = "Native host core of the MI355X tree-search engine (Taillard, bounds, pools, CPU drivers).";
   bind_engine(m);
+  bind_runner(m);
 
   // ---- Taillard ----
   m.def("taillard_jobs", &taillard_jobs);

@@ -8,6 +8,8 @@
 #include <climits>
 #include <string>
 
+#include "../core/cpu_engine.hpp"
+#include "../core/problems.hpp"
 #include "../hip/pfsp_engine.hpp"
 #include "../hip/queens_engine.hpp"
 #include "engine_binding.hpp"
@@ -37,6 +39,28 @@ EngineConfig make_cfg(int device, size_t max_parents, size_t ring_bytes, int ite
 PYBIND11_MODULE(_tts_hip, m) {
   m.doc() = "gfx950 (MI355X) device engines: device-resident pools, fused bound/prune/compact kernels, hipGraphs.";
   bind_engine(m);
+  bind_runner(m);
+
+  // CPU workers that can be mixed with GPU engines in run_workers (-C 1)
+  m.def(
+      "make_pfsp_cpu_engine",
+      [](int jobs, int machines, std::vector<int> p, int lb, size_t batch, int threads) -> std::unique_ptr<IEngine> {
+        auto inst = std::make_shared<PfspInstance>(make_instance(jobs, machines, std::move(p)));
+        return with_pfsp_bucket(jobs, [&](auto nj) -> std::unique_ptr<IEngine> {
+          constexpr int NJ = decltype(nj)::value;
+          // LB1 is evaluated with the incremental LB1_d on the CPU (same values)
+          return std::make_unique<OwningCpuEngine<PfspProblem<NJ>>>(inst, PfspProblem<NJ>(*inst, lb == 1 ? 0 : lb),
+                                                                     batch, threads);
+        });
+      },
+      py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("batch") = 4096,
+      py::arg("threads") = 1);
+  m.def(
+      "make_queens_cpu_engine",
+      [](int N, int G, size_t batch, int threads) -> std::unique_ptr<IEngine> {
+        return std::make_unique<CpuEngine<QueensProblem>>(QueensProblem(N, G), batch, threads);
+      },
+      py::arg("N"), py::arg("G") = 1, py::arg("batch") = 4096, py::arg("threads") = 1);
 
   m.def("device_count", []() {
     int n = 0;

@@ -10,10 +10,12 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 
 #include "engine_api.hpp"
+#include "pfsp_instance.hpp"
 #include "search_cpu.hpp"
 
 namespace tts {
@@ -129,6 +131,35 @@ class CpuEngine final : public IEngine {
   int best_ = 0x7fffffff;
   u64 tree_ = 0, sol_ = 0, parents_ = 0, launches_ = 0;
   double t_run_ = 0;
+};
+
+// CPU engine that keeps its PFSP instance alive (for callers that build the
+// instance on the fly, e.g. the HIP module's CPU workers).
+template <class Problem>
+class OwningCpuEngine final : public IEngine {
+ public:
+  OwningCpuEngine(std::shared_ptr<const PfspInstance> inst, Problem prob, size_t batch, int threads)
+      : inst_(std::move(inst)), eng_(std::move(prob), batch, threads) {}
+  size_t node_bytes() const override { return eng_.node_bytes(); }
+  void push_host(const void* n, size_t k) override { eng_.push_host(n, k); }
+  size_t pop_host(void* o, size_t k) override { return eng_.pop_host(o, k); }
+  size_t export_device(void* d, size_t k) override { return eng_.export_device(d, k); }
+  void import_device(const void* s, size_t k) override { eng_.import_device(s, k); }
+  size_t size() override { return eng_.size(); }
+  long run(long a, double b, size_t c) override { return eng_.run(a, b, c); }
+  void begin(const void* n, size_t k, int b) override { eng_.begin(n, k, b); }
+  EngineStats solve_from(const void* n, size_t k, int b) override { return eng_.solve_from(n, k, b); }
+  void set_best(int b) override { eng_.set_best(b); }
+  int best() override { return eng_.best(); }
+  void reset_counters() override { eng_.reset_counters(); }
+  EngineStats stats() override { return eng_.stats(); }
+  void synchronize() override {}
+  uintptr_t stream() const override { return 0; }
+  int device() const override { return -1; }
+
+ private:
+  std::shared_ptr<const PfspInstance> inst_;
+  CpuEngine<Problem> eng_;
 };
 
 }  // namespace tts

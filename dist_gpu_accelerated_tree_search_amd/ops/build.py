@@ -85,9 +85,15 @@ def build_cli(newest: float, jobs: int, with_hip: bool = True) -> list[Path]:
             out = BIN / name
             if src.exists() and _stale(out, newest):
                 objs = [str(o) for o in _hip_objects(newest, jobs)]
-                tasks.append([HIPCC, *HIPFLAGS, "-pthread", str(src), *objs, "-o", str(out)])
+                app_o = OBJ / f"app_{name}.o"
+                tasks.append([[HIPCC, *HIPFLAGS, "-pthread", "-c", str(src), "-o", str(app_o)],
+                              [HIPCC, f"--offload-arch={ARCH}", "-pthread", str(app_o), *objs, "-o", str(out)]])
+    def run_task(t):
+        for c in (t if isinstance(t[0], list) else [t]):
+            _run(c)
+
     with ThreadPoolExecutor(max_workers=jobs) as ex:
-        list(ex.map(_run, tasks))
+        list(ex.map(run_task, tasks))
     return [BIN / n for n in ("pfsp_c", "pfsp_omp_c", "nqueens_c", "pfsp_gpu", "nqueens_gpu")]
 
 

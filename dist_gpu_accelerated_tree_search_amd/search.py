@@ -99,3 +99,52 @@ def solve_gpu(model, ub: int = 1, device: int = 0, m: int = 25, opts: EngineOpti
         return solve_engine(model, eng, ub=ub, m=m, verbose=verbose)
     finally:
         del eng
+
+
+def solve_workers(model, devices=(0,), cpu_threads: int = 0, ub: int = 1, m: int = 25, steal_cap: int = 250000,
+                  ws: bool = True, opts: EngineOptions | None = None, engines=None, slice_min: float = 0.0005,
+                  slice_max: float = 0.05) -> SolveResult:
+    """Several engines in ONE process — GPUs (`devices`, repeats allowed) plus an
+    optional CPU worker with `cpu_threads` threads (-C 1) — driven by the native
+    runner (csrc/core/runner.hpp), the analogue of ref pfsp_multigpu_cuda.c.
+    Pass `engines` to reuse engines across solves."""
+    gpu = len(devices) > 0
+    mod = ops.require_gpu(max(devices)) if gpu else ops.cpu()
+    if engines is None:
+        engines = [model.make_engine("gpu", d, opts) for d in devices]
+        if cpu_threads > 0:
+            engines.append(_cpu_worker(model, mod, cpu_threads, opts))
+    W = len(engines)
+    if W == 0:
+        raise ValueError("no worker")
+    t0 = time.perf_counter()
+    best = model.initial_best(ub)
+    nodes, tree1, sol1, best = model.warmup(best, W * m)
+    from .parallel.runtime import round_robin_share
+
+    init = [np.ascontiguousarray(nodes[round_robin_share(len(nodes), w, W)]) for w in range(W)]
+    t1 = time.perf_counter()
+    out = mod.run_workers(engines, init, int(best), m=m, steal_cap=steal_cap, slice_min=slice_min,
+                          slice_max=slice_max, ws=ws)
+    t2 = time.perf_counter()
+    ws_ = out["workers"]
+    tree = tree1 + sum(int(w["tree"]) for w in ws_)
+    sol = sol1 + sum(int(w["sol"]) for w in ws_)
+    workers = [WorkerStats(tree=int(w["tree"]), sol=int(w["sol"]), gen_child=int(w["tree"]),
+                           steals=int(w["transfers_in"]), success_steals=int(w["transfers_in"]),
+                           terminations=int(w["rounds"]), t_memcpy=float(w["t_memcpy"]),
+                           t_malloc=float(w["t_malloc"]), t_kernel=float(w["t_run_w"]),
+                           t_pool_ops=float(w["t_comm"]), t_idle=float(w["t_idle"])) for w in ws_]
+    return SolveResult(best=min(int(best), int(out["best"])), tree=tree, sol=sol, elapsed=t2 - t0,
+                       t_init=t1 - t0, t_search=t2 - t1, workers=workers,
+                       extra={"rounds": max(int(w["rounds"]) for w in ws_), "engines": engines,
+                              "sent_nodes": [int(w["sent"]) for w in ws_]})
+
+
+def _cpu_worker(model, mod, threads: int, opts: EngineOptions | None):
+    batch = (opts or EngineOptions()).cpu_batch
+    if model.kind == "pfsp":
+        return mod.make_pfsp_cpu_engine(model.jobs, model.machines, list(model.native.p), model.lb, batch, threads) \
+            if hasattr(mod, "make_pfsp_engine") else mod.make_pfsp_cpu_engine(model.native, model.host_lb, batch,
+                                                                              threads)
+    return mod.make_queens_cpu_engine(model.N, model.G, batch, threads)

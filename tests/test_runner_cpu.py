@@ -1,0 +1,93 @@
+"""Native single-process multi-worker runner (csrc/core/runner.hpp) with CPU engines.
+
+Parity: ref pfsp_multigpu_cuda.c (one thread per device + optional CPU worker,
+steal-half sharing, incumbent sharing, termination). Lost or duplicated nodes in
+the round protocol show up as a wrong golden tree."""
+import subprocess
+
+import pytest
+
+from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel, QueensModel, ops
+from dist_gpu_accelerated_tree_search_amd.search import solve_workers
+
+OPTS = EngineOptions(cpu_batch=512)
+
+
+def _cpu_engines(model, n, threads=1):
+    C = ops.cpu()
+    if model.kind == "pfsp":
+        return [C.make_pfsp_cpu_engine(model.native, model.host_lb, 512, threads) for _ in range(n)]
+    return [C.make_queens_cpu_engine(model.N, model.G, 512, threads) for _ in range(n)]
+
+
+@pytest.mark.parametrize("W", [1, 2, 3, 4])
+def test_runner_pfsp_golden(W):
+    model = PfspModel(14, 1)
+    r = solve_workers(model, devices=(), engines=_cpu_engines(model, W))
+    assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377)
+    assert len(r.workers) == W
+    if W > 1:  # work actually moved between workers
+        assert sum(r.extra["sent_nodes"]) > 0
+
+
+def test_runner_lb2_and_no_sharing():
+    model = PfspModel(14, 2)
+    r = solve_workers(model, devices=(), engines=_cpu_engines(model, 3))
+    assert (r.tree, r.sol, r.best) == (144639, 0, 1377)
+    model = PfspModel(14, 0)
+    r = solve_workers(model, devices=(), engines=_cpu_engines(model, 2), ws=False)
+    assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377)
+    assert sum(r.extra["sent_nodes"]) == 0
+
+
+def test_runner_unknown_optimum_shares_incumbent():
+    model = PfspModel.synthetic(8, 5, seed=3, lb=1)
+    import itertools
+
+    import numpy as np
+
+    p = np.asarray(model.native.p).reshape(5, 8)
+
+    def cmax(perm):
+        c = [0] * 5
+        for j in perm:
+            for k in range(5):
+                c[k] = max(c[k], c[k - 1] if k else 0) + int(p[k, j])
+        return c[-1]
+
+    opt = min(cmax(q) for q in itertools.permutations(range(8)))
+    r = solve_workers(model, devices=(), engines=_cpu_engines(model, 3), ub=0, m=4)
+    assert r.best == opt
+
+
+def test_runner_queens_and_engine_reuse():
+    model = QueensModel(11)
+    engines = _cpu_engines(model, 3)
+    for _ in range(2):
+        r = solve_workers(model, devices=(), engines=engines)
+        assert (r.tree, r.sol) == (166925, 2680)
+
+
+def test_runner_cpu_worker_helper():
+    # devices=() + cpu_threads builds one multithreaded CPU engine (-D 0 -C 1)
+    r = solve_workers(PfspModel(14, 1), devices=(), cpu_threads=2, opts=OPTS)
+    assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377)
+
+
+def test_runner_rejects_mixed_layouts():
+    a = PfspModel(14, 1)  # 20 jobs -> 32-B nodes
+    C = ops.cpu()
+    engines = [C.make_pfsp_cpu_engine(a.native, 0, 512, 1), C.make_queens_cpu_engine(8, 1, 512, 1)]
+    with pytest.raises(Exception):
+        C.run_workers(engines, [a.root(), a.root()[:0].reshape(0, 16)], 1377)
+
+
+def test_native_gpu_cli_fails_cleanly_without_device():
+    from dist_gpu_accelerated_tree_search_amd.ops.build import BIN
+
+    exe = BIN / "pfsp_gpu"
+    if not exe.exists() or ops.gpu_count() > 0:
+        pytest.skip("needs the built CLI on a host without GPUs")
+    out = subprocess.run([str(exe), "-i", "14", "-l", "1", "-D", "1"], capture_output=True, text=True, timeout=60)
+    assert out.returncode != 0
+    assert "More GPU devices requested" in out.stdout
