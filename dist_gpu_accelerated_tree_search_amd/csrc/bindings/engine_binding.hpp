@@ -69,6 +69,10 @@ inline void bind_engine(py::module_& m) {
           py::arg("ptr"), py::arg("n"), py::call_guard<py::gil_scoped_release>(),
           "Append n nodes read from device memory at ptr.")
       .def("size", &IEngine::size, py::call_guard<py::gil_scoped_release>())
+      .def("warm_split", &IEngine::warm_split, py::arg("rank"), py::arg("world"), py::arg("window") = 4096,
+           py::arg("passes") = 1, py::call_guard<py::gil_scoped_release>(),
+           "Redundant deterministic warm-up (passes x 6 steps, parent window) then keep the i % world == rank "
+           "share of the pool; warm-up counters stay on rank 0. Returns the kept pool size.")
       .def("run", &IEngine::run, py::arg("max_launches") = -1, py::arg("max_seconds") = 0.0,
            py::arg("stop_below") = 0, py::call_guard<py::gil_scoped_release>())
       .def(

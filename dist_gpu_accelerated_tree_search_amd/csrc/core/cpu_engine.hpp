@@ -85,6 +85,27 @@ class CpuEngine final : public IEngine {
     return stats();
   }
 
+  size_t warm_split(int rank, int world, size_t window, int passes) override {
+    const double t0 = now_s();
+    std::vector<Node> parents(std::max<size_t>(1, window));
+    for (int i = 0; i < passes * 6 && !pool_.empty(); ++i) {
+      const size_t n = pool_.pop_back_bulk_free(1, parents.size(), parents.data(), 1);
+      expand(parents.data(), n);
+      parents_ += n;
+      ++launches_;
+    }
+    if (world > 1) {
+      std::vector<Node> mine;
+      const size_t n = pool_.size();
+      for (size_t i = static_cast<size_t>(rank); i < n; i += static_cast<size_t>(world)) mine.push_back(pool_.data()[i]);
+      pool_.clear();
+      pool_.push_back_bulk_free(mine.data(), mine.size());
+      if (rank != 0) reset_counters();
+    }
+    t_run_ += now_s() - t0;
+    return pool_.size();
+  }
+
   EngineStats stats() override {
     EngineStats s;
     s.tree = tree_;
@@ -149,6 +170,7 @@ class OwningCpuEngine final : public IEngine {
   long run(long a, double b, size_t c) override { return eng_.run(a, b, c); }
   void begin(const void* n, size_t k, int b) override { eng_.begin(n, k, b); }
   EngineStats solve_from(const void* n, size_t k, int b) override { return eng_.solve_from(n, k, b); }
+  size_t warm_split(int r, int w, size_t win, int p) override { return eng_.warm_split(r, w, win, p); }
   void set_best(int b) override { eng_.set_best(b); }
   int best() override { return eng_.best(); }
   void reset_counters() override { eng_.reset_counters(); }

@@ -44,6 +44,13 @@ class IEngine {
   virtual void begin(const void* nodes, size_t n, int best) = 0;
   // One complete solve from `n` nodes with incumbent `best` (begin + run + stats).
   virtual EngineStats solve_from(const void* nodes, size_t n, int best) = 0;
+  // Deterministic redundant warm start of a multi-rank solve: every rank has
+  // begun from the same nodes with the same configuration; `passes` x 6
+  // expansion steps with a parent window of `window` grow a wide frontier, then
+  // the rank keeps the pool elements i with i % world == rank (bottom first).
+  // Counters of the redundant phase are kept by rank 0 only, so the sum over
+  // ranks is the explored tree. Returns the pool size kept.
+  virtual size_t warm_split(int rank, int world, size_t window, int passes) = 0;
   virtual void set_best(int b) = 0;
   virtual int best() = 0;
   virtual void reset_counters() = 0;

@@ -288,6 +288,68 @@ class DeviceEngine final : public IEngine {
     return stats();
   }
 
+  size_t warm_split(int rank, int world, size_t window, int passes) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
+    const auto t0 = std::chrono::steady_clock::now();
+    sync_ctl();
+    // 6-iteration passes with a narrower parent window (plain launches: the
+    // window is a kernel argument); identical on every rank
+    const size_t win = std::max<size_t>(1, std::min(window, cfg_.max_parents));
+    for (int p = 0; p < passes; ++p) {
+      if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
+      const size_t total = dev_total();
+      if (total == 0 || total + 7 * buf_nodes_ > cap_) break;
+      auto a = args_;
+      a.pool.max_parents = static_cast<int>(win);
+      a.pool.max_chunks = static_cast<int>((win + Traits::kParentsPerChunk - 1) / Traits::kParentsPerChunk);
+      const int m = next_mirror_;
+      next_mirror_ ^= 1;
+      for (int i = 0; i < 6; ++i) Traits::launch(a, i, grid_, stream_);
+      a.pool.mirror = d_mirror_[m];
+      Traits::finalize(a.pool, stream_);
+      TTS_HIP_CHECK(hipGetLastError());
+      TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
+      inflight_.push_back(m);
+      inflight_k_.push_back(0);
+      ++stats_.launches;
+      sync_ctl();
+    }
+    if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
+    normalize();
+    if (world > 1) {
+      // strided share of the device part, then of the host spill
+      const size_t n = dev_stack();
+      const size_t keep = n > static_cast<size_t>(rank) ? (n - rank + world - 1) / world : 0;
+      if (keep) {
+        Node* tmp = d_buf_[1];
+        if (keep > buf_nodes_) TTS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&tmp), keep * sizeof(Node)));
+        const int vpn = static_cast<int>(sizeof(Node) / 16);
+        const int blocks = static_cast<int>(std::min<size_t>((keep * vpn + dev::kBlock - 1) / dev::kBlock, 4096));
+        hipLaunchKernelGGL(dev::pool_gather_strided_kernel<Node>, dim3(blocks), dim3(dev::kBlock), 0, stream_, d_ring_,
+                           static_cast<dev::u64>(cap_ - 1), static_cast<dev::u64>(h_ctl_->bot), static_cast<dev::u64>(keep), rank,
+                           world, tmp);
+        TTS_HIP_CHECK(hipGetLastError());
+        TTS_HIP_CHECK(hipMemcpyAsync(d_ring_, tmp, keep * sizeof(Node), hipMemcpyDeviceToDevice, stream_));
+        if (tmp != d_buf_[1]) {
+          TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+          TTS_HIP_CHECK(hipFree(tmp));
+        }
+      }
+      h_ctl_->bot = 0;
+      h_ctl_->stack[0].v = keep;
+      if (!spill_.empty()) {
+        std::vector<Node> mine;
+        for (size_t i = rank; i < spill_.size(); i += world) mine.push_back(spill_[i]);
+        spill_.swap(mine);
+      }
+      if (rank != 0) h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
+      upload_ctl();
+    }
+    stats_.t_run += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return dev_total() + spill_.size();
+  }
+
   void set_best(int b) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();

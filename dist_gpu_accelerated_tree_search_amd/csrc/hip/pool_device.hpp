@@ -187,6 +187,22 @@ __global__ __launch_bounds__(kBlock) void pool_flatten_kernel(PoolArgs<Node> pa)
   pool_spill_leftovers<Node, MAXCH, MAXCHUNKS>(pa, v, 0, ps);
 }
 
+// Rank share of a replicated pool: out[t] = ring[bot + rank + t*world], t < keep
+// (a strided pick gives every rank a sample of every subtree of the frontier).
+template <class Node>
+__global__ __launch_bounds__(kBlock) void pool_gather_strided_kernel(const Node* __restrict__ ring, u64 cap_mask,
+                                                                     u64 bot, u64 keep, int rank, int world,
+                                                                     Node* __restrict__ out) {
+  constexpr int VPN = sizeof(Node) / 16;
+  for (u64 x = static_cast<u64>(blockIdx.x) * kBlock + threadIdx.x; x < keep * VPN;
+       x += static_cast<u64>(gridDim.x) * kBlock) {
+    const u64 t = x / VPN;
+    const int w = static_cast<int>(x - t * VPN);
+    const Node* src = ring + ((bot + static_cast<u64>(rank) + t * static_cast<u64>(world)) & cap_mask);
+    reinterpret_cast<uint4*>(out + t)[w] = reinterpret_cast<const uint4*>(src)[w];
+  }
+}
+
 // Last node of every graph: counts of the latest buffer for the host.
 template <class Node, int MAXCHUNKS>
 __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa) {

@@ -39,6 +39,12 @@ class DistConfig:
     slice_max_s: float = 0.050
     ws: bool = True              # share within a node (ref -w)
     L: bool = True               # share across nodes (ref -L)
+    # Step 1 on the engines instead of the host: every rank expands the root with
+    # the same deterministic warm-up (warm_passes x 6 steps, warm_window parents
+    # per step) and keeps the i % world == rank share of the resulting frontier.
+    engine_warmup: bool = True
+    warm_window: int = 2048
+    warm_passes: int = 1
     verbose: bool = False
 
 
@@ -75,8 +81,15 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
     world, rank = comm.world, comm.rank
     t_start = time.perf_counter()
 
-    # ---- Step 1: redundant, deterministic host warm-up on every rank ----
+    # ---- Step 1: redundant, deterministic warm-up on every rank ----
     best = model.initial_best(ub)
+    if world > 1 and cfg.engine_warmup:
+        # on the engine: wide frontier in a few device iterations, strided share
+        tree1 = sol1 = 0
+        engine.begin(model.root(), int(best))
+        engine.warm_split(rank, world, cfg.warm_window, cfg.warm_passes)
+        rs.t_init = time.perf_counter() - t_start
+        return _rounds(model, engine, comm, cfg, rs, t_start, best, tree1, sol1)
     nodes, tree1, sol1, best = model.warmup(best, world * cfg.init_per_rank)
     mine = np.ascontiguousarray(nodes[round_robin_share(len(nodes), rank, world)])
     rs.t_init = time.perf_counter() - t_start
@@ -90,6 +103,13 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
                            t_search=elapsed - rs.t_init, workers=[w],
                            extra={"rounds": 0, "sent_nodes": [0], "received_nodes": [0], "world": 1})
     engine.begin(mine, int(best))
+    return _rounds(model, engine, comm, cfg, rs, t_start, best, tree1, sol1)
+
+
+def _rounds(model, engine, comm: Comm, cfg: DistConfig, rs: RankStats, t_start: float, best: int, tree1: int,
+            sol1: int) -> SolveResult:
+    """Step 2 (lock-step rounds until every pool is empty) and the final reductions."""
+    world, rank = comm.world, comm.rank
 
     # ---- Step 2: rounds ----
     share = cfg.ws or cfg.L
@@ -132,11 +152,12 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
     st = engine.stats()
     rs.tree, rs.sol = int(st["tree"]), int(st["sol"])
     best_local = min(int(st["best"]), int(best))
-    tot = comm.allreduce_i64([rs.tree + (tree1 if rank == 0 else 0), rs.sol + (sol1 if rank == 0 else 0)], "sum")
-    gbest = int(comm.allreduce_i64([best_local], "min")[0])
+    # one collective for every final reduction (counts < 2^53 are exact in f64)
     per = comm.allgather_f64([rs.tree, rs.sol, rs.sent, rs.received, rs.transfers_in, rs.transfers_out,
                               rs.rounds, rs.t_run, rs.t_comm, rs.t_idle, rs.t_init,
-                              float(st.get("t_memcpy", 0.0)), float(st.get("t_malloc", 0.0))])
+                              float(st.get("t_memcpy", 0.0)), float(st.get("t_malloc", 0.0)), best_local])
+    tot = (int(round(sum(float(r[0]) for r in per))) + tree1, int(round(sum(float(r[1]) for r in per))) + sol1)
+    gbest = int(min(float(r[13]) for r in per))
     elapsed = time.perf_counter() - t_start
     workers = [WorkerStats(tree=int(r[0]), sol=int(r[1]), gen_child=int(r[0]), steals=int(r[4]),
                            success_steals=int(r[4]), terminations=int(r[6]), t_memcpy=float(r[11]),

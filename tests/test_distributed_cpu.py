@@ -43,9 +43,12 @@ def test_plan_sharing_properties():
     assert all(d == 1 for d, _, _ in p)
 
 
-@pytest.mark.parametrize("world,ws,lb", [(2, True, 0), (3, True, 1), (4, True, 0), (3, False, 0)])
-def test_pfsp_golden_tree(world, ws, lb):
-    spec = {"problem": "pfsp", "inst": 14, "lb": lb, "backend": "cpu", "dist": {"ws": ws, "L": ws}}
+@pytest.mark.parametrize("world,ws,lb,ew", [(2, True, 0, True), (3, True, 1, True), (4, True, 0, True),
+                                           (3, False, 0, True), (3, True, 0, False), (2, False, 1, False)])
+def test_pfsp_golden_tree(world, ws, lb, ew):
+    # ew: Step 1 on the engines (warm_split) or on the host (BFS + round-robin)
+    spec = {"problem": "pfsp", "inst": 14, "lb": lb, "backend": "cpu",
+            "dist": {"ws": ws, "L": ws, "engine_warmup": ew}}
     res = spawn_local(world, solve_rank, (spec,), timeout=300)
     for r in res:
         assert (r["tree"], r["sol"], r["best"]) == GOLD
@@ -72,6 +75,32 @@ def test_queens_and_stress_small_thresholds():
     res = spawn_local(4, solve_rank, (spec,), timeout=300)
     assert (res[0]["tree"], res[0]["sol"]) == (166925, 2680)
     assert res[0]["extra"]["rounds"] > 1
+
+
+def test_warm_split_partitions_the_frontier():
+    # every rank runs the same warm-up; the shares are disjoint and cover the pool
+    import numpy as np
+
+    from dist_gpu_accelerated_tree_search_amd import PfspModel, ops
+
+    model = PfspModel(14, 1)
+    C = ops.cpu()
+
+    def frontier(rank, world):
+        e = C.make_pfsp_cpu_engine(model.native, 0, 64, 1)
+        e.begin(model.root(), 1377)
+        n = e.warm_split(rank, world, 64, 1)
+        nodes = e.pop(n)
+        return e, nodes
+
+    full_e, full = frontier(0, 1)
+    world = 3
+    shares = [frontier(r, world) for r in range(world)]
+    assert sum(len(s[1]) for s in shares) == len(full)
+    for r, (e, nodes) in enumerate(shares):
+        assert np.array_equal(nodes, full[r::world])
+        st = e.stats()
+        assert (st["tree"] > 0) == (r == 0)  # warm-up counted once
 
 
 def test_repeated_solves_reuse_engine():

@@ -81,3 +81,34 @@ def test_push_pop_export_import_roundtrip():
     eng.run()
     st = eng.stats()
     assert (st["tree"] + tree1, st["sol"] + sol1) == (2573652, 2648)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_warm_split_on_device(world):
+    model = PfspModel(14, 1)
+    opts = EngineOptions(ring_bytes=1 << 30)
+
+    def share(rank, w):
+        e = model.make_engine("gpu", 0, opts)
+        e.begin(model.root(), 1377)
+        n = e.warm_split(rank, w, 1024, 1)
+        st = e.stats()
+        return n, e.pop(n), st, e
+
+    n_full, full, st_full, _ = share(0, 1)
+    got = [share(r, world) for r in range(world)]
+    assert sum(g[0] for g in got) == n_full
+    for r, (n, nodes, st, _) in enumerate(got):
+        assert np.array_equal(nodes, full[r::world])
+        assert (st["tree"] == st_full["tree"]) if r == 0 else st["tree"] == 0
+    # the shares solve to the golden tree in total
+    tree = sol = 0
+    for r in range(world):
+        e = model.make_engine("gpu", 0, opts)
+        e.begin(model.root(), 1377)
+        e.warm_split(r, world, 1024, 1)
+        e.run()
+        st = e.stats()
+        tree += st["tree"]
+        sol += st["sol"]
+    assert (tree, sol) == GOLDEN[(14, 1)][:2]
