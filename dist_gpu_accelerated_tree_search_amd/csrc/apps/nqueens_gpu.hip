@@ -5,11 +5,13 @@
 
 #include "../core/drivers_cpu.hpp"
 #include "../core/runner.hpp"
+#include "../hip/host_support.hpp"
 #include "../hip/queens_engine.hpp"
 
 using namespace tts;
 
 int main(int argc, char* argv[]) {
+  install_roctx_hooks();
   const QueensArgs a = parse_queens_args(argc, argv, true);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
@@ -48,7 +50,10 @@ int main(int argc, char* argv[]) {
   RunnerConfig rc;
   rc.m = a.m;
   rc.steal_cap = static_cast<size_t>(5) * a.M;
-  const auto rep = run_workers(engines, init, best, rc);
+  rc.merge_env();
+  for (auto* e : engines) rc.worker_cpus.push_back(device_cpus(e->device()));
+  HipStaging staging;
+  const auto rep = run_workers(engines, init, best, rc, &staging);
   for (auto& r : rep) {
     tree += r.st.tree;
     sol += r.st.sol;

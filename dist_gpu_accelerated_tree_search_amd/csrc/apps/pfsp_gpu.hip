@@ -10,11 +10,13 @@
 #include "../core/cpu_engine.hpp"
 #include "../core/drivers_cpu.hpp"
 #include "../core/runner.hpp"
+#include "../hip/host_support.hpp"
 #include "../hip/pfsp_engine.hpp"
 
 using namespace tts;
 
 int main(int argc, char* argv[]) {
+  install_roctx_hooks();
   PfspArgs a = parse_pfsp_args(argc, argv);
   if (a.C < 0 || a.C > 1) {
     std::printf("C is set to %d. Invalid option for this version.\nChoose 0 to unable and 1 to enable multi-core. "
@@ -84,7 +86,10 @@ int main(int argc, char* argv[]) {
     rc.m = a.m;
     rc.steal_cap = static_cast<size_t>(5) * a.M;
     rc.work_sharing = a.ws == 1;
-    const auto rep = run_workers(engines, init, best, rc);
+    rc.merge_env();
+    for (auto* e : engines) rc.worker_cpus.push_back(e->device() >= 0 ? device_cpus(e->device()) : std::vector<int>{});
+    HipStaging staging;
+    const auto rep = run_workers(engines, init, best, rc, &staging);
     std::vector<WorkerStats> ws(W);
     for (int w = 0; w < W; ++w) {
       tree += rep[w].st.tree;

@@ -5,8 +5,12 @@
 
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <pybind11/functional.h>
 
+#include <functional>
 #include <memory>
+#include <vector>
 #include <stdexcept>
 
 #include "../core/engine_api.hpp"
@@ -103,12 +107,18 @@ inline void bind_engine(py::module_& m) {
 }
 
 // run_workers(engines, initial_nodes, best, ...) -> {"best": int, "workers": [dict]}
-inline void bind_runner(py::module_& m) {
+// `staging` (HIP module only) enables device-to-device steals between GPU engines;
+// `cpus_of_device` maps a GPU to its NUMA-local CPUs for thread pinning.
+using StagingFactory = std::function<std::unique_ptr<DeviceStaging>()>;
+using CpusOfDevice = std::function<std::vector<int>(int)>;
+
+inline void bind_runner(py::module_& m, StagingFactory staging = {}, CpusOfDevice cpus_of_device = {}) {
   using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
   m.def(
       "run_workers",
-      [](py::list engines, py::list initial, int best, size_t m_, size_t steal_cap, double slice_min, double slice_max,
-         bool ws) {
+      [staging, cpus_of_device](py::list engines, py::list initial, int best, size_t m_, size_t steal_cap,
+                                double slice_min, double slice_max, bool ws, bool pin, bool device_steals,
+                                double watchdog_s, py::dict faults) {
         if (engines.size() != initial.size()) throw std::invalid_argument("one initial node array per engine");
         std::vector<IEngine*> es;
         std::vector<std::vector<uint8_t>> init;
@@ -126,10 +136,21 @@ inline void bind_runner(py::module_& m) {
         cfg.slice_min = slice_min;
         cfg.slice_max = slice_max;
         cfg.work_sharing = ws;
+        cfg.watchdog_s = watchdog_s;
+        cfg.merge_env();
+        if (faults.contains("delay_us")) cfg.fault_delay_us = faults["delay_us"].cast<unsigned>();
+        if (faults.contains("steal_fail_pct")) cfg.fault_steal_fail_pct = faults["steal_fail_pct"].cast<unsigned>();
+        if (faults.contains("stall_worker")) cfg.fault_stall_worker = faults["stall_worker"].cast<int>();
+        if (faults.contains("stall_s")) cfg.fault_stall_s = faults["stall_s"].cast<double>();
+        if (faults.contains("seed")) cfg.fault_seed = faults["seed"].cast<unsigned long long>();
+        if (pin && cpus_of_device)
+          for (auto* e : es) cfg.worker_cpus.push_back(e->device() >= 0 ? cpus_of_device(e->device()) : std::vector<int>{});
+        std::unique_ptr<DeviceStaging> st;
+        if (device_steals && staging) st = staging();
         std::vector<WorkerReport> rep;
         {
           py::gil_scoped_release nogil;
-          rep = run_workers(es, init, best, cfg);
+          rep = run_workers(es, init, best, cfg, st.get());
         }
         py::list ws_out;
         for (auto& r : rep) {
@@ -139,6 +160,10 @@ inline void bind_runner(py::module_& m) {
           d["received"] = r.received;
           d["transfers_in"] = r.transfers_in;
           d["transfers_out"] = r.transfers_out;
+          d["device_transfers"] = r.device_transfers;
+          d["dropped_transfers"] = r.dropped_transfers;
+          d["watchdog_events"] = r.watchdog_events;
+          d["pinned"] = r.pinned;
           d["t_run_w"] = r.t_run;
           d["t_comm"] = r.t_comm;
           d["t_idle"] = r.t_idle;
@@ -150,8 +175,11 @@ inline void bind_runner(py::module_& m) {
         return out;
       },
       py::arg("engines"), py::arg("initial"), py::arg("best"), py::arg("m") = 25, py::arg("steal_cap") = 250000,
-      py::arg("slice_min") = 0.0005, py::arg("slice_max") = 0.05, py::arg("ws") = true,
+      py::arg("slice_min") = 0.0005, py::arg("slice_max") = 0.05, py::arg("ws") = true, py::arg("pin") = false,
+      py::arg("device_steals") = true, py::arg("watchdog_s") = 0.0, py::arg("faults") = py::dict(),
       "Drive several engines (GPUs and/or CPU workers) from one process until all pools are empty.");
+  m.def("parse_cpulist", &parse_cpulist);
+  m.def("allowed_cpus", &allowed_cpus);
 }
 
 }  // namespace tts

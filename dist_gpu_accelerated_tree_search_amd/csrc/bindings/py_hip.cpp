@@ -10,6 +10,7 @@
 
 #include "../core/cpu_engine.hpp"
 #include "../core/problems.hpp"
+#include "../hip/host_support.hpp"
 #include "../hip/pfsp_engine.hpp"
 #include "../hip/queens_engine.hpp"
 #include "engine_binding.hpp"
@@ -39,7 +40,11 @@ EngineConfig make_cfg(int device, size_t max_parents, size_t ring_bytes, int ite
 PYBIND11_MODULE(_tts_hip, m) {
   m.doc() = "gfx950 (MI355X) device engines: device-resident pools, fused bound/prune/compact kernels, hipGraphs.";
   bind_engine(m);
-  bind_runner(m);
+  bind_runner(
+      m, []() -> std::unique_ptr<DeviceStaging> { return std::make_unique<HipStaging>(); }, &device_cpus);
+  if (!std::getenv("TTS_NO_ROCTX")) install_roctx_hooks();
+  m.def("device_pci_bus_id", &device_pci_bus_id);
+  m.def("device_cpus", &device_cpus, "CPUs of the NUMA node closest to the GPU (empty if unknown).");
 
   // CPU workers that can be mixed with GPU engines in run_workers (-C 1)
   m.def(

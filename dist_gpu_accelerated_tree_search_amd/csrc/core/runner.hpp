@@ -8,24 +8,37 @@
 //   * a round = barrier -> leader reads every pool size + incumbent, takes the
 //     MIN incumbent, detects termination (all pools empty: exact, nothing is in
 //     flight between rounds), plans steal-half transfers (same plan as
-//     parallel/comm.py::plan_sharing) -> barrier -> donors move nodes into
-//     staging -> barrier -> receivers load them -> next slice.
-// The multi-process equivalent over RCCL is parallel/runtime.py; this runner is
-// the native path (no Python, no collectives library) for one node.
+//     parallel/comm.py::plan_sharing) -> barrier -> donors move nodes -> barrier
+//     -> receivers load them -> next slice.
+//   * GPU -> GPU transfers go device pool -> staging buffer on the receiver's
+//     device (peer copy over xGMI, DeviceStaging) -> receiver pool; transfers that
+//     involve a CPU worker are staged through host memory.
+// Aux subsystems: host threads pinned to the NUMA node of their GPU,
+// a watchdog that reports (and optionally aborts) a stuck phase, env-driven fault
+// injection (TTS_FAULT_DELAY_US, TTS_FAULT_STEAL_FAIL_PCT, TTS_FAULT_STALL), and
+// named trace ranges (roctx when the HIP module installs it).
+// The multi-process equivalent over RCCL is parallel/runtime.py.
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <mutex>
+#include <random>
+#include <string>
 #include <thread>
 #include <tuple>
 #include <vector>
 
 #include "engine_api.hpp"
+#include "topology.hpp"
+#include "trace.hpp"
 
 namespace tts {
 
@@ -35,12 +48,52 @@ struct RunnerConfig {
   double slice_min = 0.0005;   // seconds of local search between rounds (adaptive)
   double slice_max = 0.05;
   bool work_sharing = true;    // ref -w
+  std::vector<std::vector<int>> worker_cpus;  // optional CPU set per worker (pinning)
+  double watchdog_s = 0;       // report a phase longer than this (0: off)
+  bool watchdog_abort = false; // abort the process after the report
+  // fault injection
+  unsigned fault_delay_us = 0;        // random extra delay per worker per round
+  unsigned fault_steal_fail_pct = 0;  // planned transfers dropped (seeded)
+  int fault_stall_worker = -1;        // this worker stalls once (round 1) ...
+  double fault_stall_s = 0;           // ... for this long
+  unsigned long long fault_seed = 12345;
+
+  // TTS_WATCHDOG_S, TTS_WATCHDOG_ABORT, TTS_FAULT_DELAY_US, TTS_FAULT_STEAL_FAIL_PCT,
+  // TTS_FAULT_STALL="worker:seconds"
+  void merge_env() {
+    auto env = [](const char* k) -> const char* {
+      const char* v = std::getenv(k);
+      return (v && *v) ? v : nullptr;
+    };
+    if (auto v = env("TTS_WATCHDOG_S")) watchdog_s = std::atof(v);
+    if (auto v = env("TTS_WATCHDOG_ABORT")) watchdog_abort = std::atoi(v) != 0;
+    if (auto v = env("TTS_FAULT_DELAY_US")) fault_delay_us = static_cast<unsigned>(std::atol(v));
+    if (auto v = env("TTS_FAULT_STEAL_FAIL_PCT")) fault_steal_fail_pct = static_cast<unsigned>(std::atol(v));
+    if (auto v = env("TTS_FAULT_STALL")) {
+      const std::string s(v);
+      const auto c = s.find(':');
+      if (c != std::string::npos) {
+        fault_stall_worker = std::atoi(s.substr(0, c).c_str());
+        fault_stall_s = std::atof(s.substr(c + 1).c_str());
+      }
+    }
+  }
 };
 
 struct WorkerReport {
   EngineStats st;
   unsigned long long rounds = 0, sent = 0, received = 0, transfers_in = 0, transfers_out = 0;
+  unsigned long long device_transfers = 0, dropped_transfers = 0, watchdog_events = 0;
   double t_run = 0, t_comm = 0, t_idle = 0;
+  bool pinned = false;
+};
+
+// Device staging buffers for GPU -> GPU transfers (implemented by the HIP side).
+class DeviceStaging {
+ public:
+  virtual ~DeviceStaging() = default;
+  virtual void* alloc(int device, size_t bytes) = 0;
+  virtual void release(int device, void* p) = 0;
 };
 
 // Deterministic steal-half matching (identical to parallel/comm.py::plan_sharing
@@ -91,29 +144,42 @@ class RoundBarrier {
   unsigned long long gen_ = 0;
 };
 
+// Worker phases seen by the watchdog.
+enum class Phase : int { Start = 0, Run = 1, Report = 2, Barrier = 3, Transfer = 4, Done = 5 };
+inline const char* phase_name(int p) {
+  static const char* n[] = {"start", "run", "report", "barrier", "transfer", "done"};
+  return (p >= 0 && p <= 5) ? n[p] : "?";
+}
+
 // Runs all workers to exhaustion. initial[w] holds worker w's starting nodes
 // (node_bytes each). Returns per-worker reports; `best` is updated to the final
 // incumbent. Engines must share one node layout.
 inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engines,
                                              const std::vector<std::vector<uint8_t>>& initial, int& best,
-                                             const RunnerConfig& cfg) {
+                                             const RunnerConfig& cfg, DeviceStaging* staging = nullptr) {
   const int W = static_cast<int>(engines.size());
   if (W == 0) return {};
+  if (initial.size() != engines.size()) throw std::invalid_argument("one initial node set per worker");
   const size_t nb = engines[0]->node_bytes();
   for (auto* e : engines)
     if (e->node_bytes() != nb) throw std::invalid_argument("workers disagree on the node layout");
   std::vector<WorkerReport> rep(W);
   std::vector<size_t> sizes(W, 0);
   std::vector<int> bests(W, best);
-  std::vector<std::vector<uint8_t>> staging(W);  // staging[r]: nodes bound for worker r
+  std::vector<std::vector<uint8_t>> staging_host(W);  // staging_host[r]: nodes bound for worker r
+  // device staging: dbuf[r] on worker r's device, written by its (single) donor
+  std::vector<void*> dbuf(W, nullptr);
+  std::vector<size_t> dcap(W, 0), dcount(W, 0);
   std::vector<std::tuple<int, int, size_t>> plan;
   bool done = false;
   int gbest = best;
   double slice = cfg.slice_min;
   RoundBarrier bar(W);
   std::mutex stage_mu;
+  std::mt19937_64 fault_rng(cfg.fault_seed);
 
-  auto now = [] { return std::chrono::steady_clock::now(); };
+  using clock = std::chrono::steady_clock;
+  auto now = [] { return clock::now(); };
   auto secs = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
 
   // A worker whose engine throws keeps taking part in the rounds with an empty
@@ -124,6 +190,46 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
     std::lock_guard<std::mutex> lk(err_mu);
     if (!err) err = p;
   };
+
+  // ---- watchdog: per-worker heartbeat {phase, round, phase start} ----
+  struct Beat {
+    std::atomic<int> phase{0};
+    std::atomic<unsigned long long> round{0};
+    std::atomic<clock::rep> since{0};
+    std::atomic<bool> reported{false};
+  };
+  std::vector<Beat> beats(W);
+  auto beat = [&](int w, Phase p) {
+    beats[w].since.store(clock::now().time_since_epoch().count(), std::memory_order_relaxed);
+    beats[w].reported.store(false, std::memory_order_relaxed);
+    beats[w].phase.store(static_cast<int>(p), std::memory_order_release);
+  };
+  std::atomic<bool> finished{false};
+  std::atomic<unsigned long long> watchdog_events{0};
+  std::thread watchdog;
+  if (cfg.watchdog_s > 0) {
+    watchdog = std::thread([&] {
+      const auto tick = std::chrono::duration<double>(std::max(0.001, cfg.watchdog_s / 4));
+      while (!finished.load()) {
+        std::this_thread::sleep_for(tick);
+        const clock::rep t = clock::now().time_since_epoch().count();
+        for (int w = 0; w < W; ++w) {
+          const int ph = beats[w].phase.load(std::memory_order_acquire);
+          if (ph == static_cast<int>(Phase::Done) || ph == static_cast<int>(Phase::Barrier)) continue;
+          const double age = std::chrono::duration<double>(clock::duration(t - beats[w].since.load())).count();
+          if (age < cfg.watchdog_s || beats[w].reported.exchange(true)) continue;
+          ++watchdog_events;
+          std::fprintf(stderr, "[tts watchdog] worker %d stuck in phase '%s' for %.3f s (round %llu); state:\n", w,
+                       phase_name(ph), age, beats[w].round.load());
+          for (int x = 0; x < W; ++x)
+            std::fprintf(stderr, "  worker %d device %d phase %s round %llu\n", x, engines[x]->device(),
+                         phase_name(beats[x].phase.load()), beats[x].round.load());
+          std::fflush(stderr);
+          if (cfg.watchdog_abort) std::abort();
+        }
+      }
+    });
+  }
 
   auto worker = [&](int w) {
     IEngine* e = engines[w];
@@ -138,18 +244,33 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
         dead = true;
       }
     };
+    if (w < static_cast<int>(cfg.worker_cpus.size()) && !cfg.worker_cpus[w].empty())
+      r.pinned = pin_current_thread(cfg.worker_cpus[w]);
+    std::mt19937 jitter(static_cast<unsigned>(cfg.fault_seed + 7919u * static_cast<unsigned>(w)));
+    beat(w, Phase::Start);
     const std::vector<uint8_t>& init = initial[w];
     guarded([&] { e->begin(init.data(), init.size() / nb, best); });
     for (;;) {
       const auto t0 = now();
-      guarded([&] { e->run(-1, slice, 1); });
+      beat(w, Phase::Run);
+      {
+        TTS_RANGE("tts.run_slice");
+        guarded([&] { e->run(-1, slice, 1); });
+      }
       const auto t1 = now();
       r.t_run += secs(t0, t1);
+      beat(w, Phase::Report);
+      if (cfg.fault_delay_us)
+        std::this_thread::sleep_for(std::chrono::microseconds(jitter() % (cfg.fault_delay_us + 1)));
+      if (w == cfg.fault_stall_worker && r.rounds == 1 && cfg.fault_stall_s > 0)
+        std::this_thread::sleep_for(std::chrono::duration<double>(cfg.fault_stall_s));
       sizes[w] = 0;
       guarded([&] {
         sizes[w] = e->size();
         bests[w] = e->best();
       });
+      beat(w, Phase::Barrier);
+      TTS_RANGE("tts.round");
       bar.wait();
       if (w == 0) {  // leader: incumbent, termination, plan
         gbest = *std::min_element(bests.begin(), bests.end());
@@ -161,45 +282,87 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
         }
         done = total == 0;
         plan.clear();
-        if (!done && cfg.work_sharing && W > 1 && starving) plan = plan_sharing(sizes, cfg.m, cfg.steal_cap);
+        if (!done && cfg.work_sharing && W > 1 && starving) {
+          plan = plan_sharing(sizes, cfg.m, cfg.steal_cap);
+          if (cfg.fault_steal_fail_pct) {
+            std::vector<std::tuple<int, int, size_t>> kept;
+            for (auto& t : plan) {
+              if (fault_rng() % 100 < cfg.fault_steal_fail_pct)
+                ++rep[std::get<1>(t)].dropped_transfers;
+              else
+                kept.push_back(t);
+            }
+            plan.swap(kept);
+          }
+        }
         slice = starving ? cfg.slice_min : std::min(cfg.slice_max, slice * 2);
       }
       bar.wait();
       ++r.rounds;
+      beats[w].round.store(r.rounds, std::memory_order_relaxed);
       if (done) {
         r.t_comm += secs(t1, now());
         break;
       }
       if (gbest < bests[w]) guarded([&] { e->set_best(gbest); });
       if (!plan.empty()) {
-        // donors: pool bottom -> staging of each receiver
+        beat(w, Phase::Transfer);
+        TTS_RANGE("tts.transfer");
+        // donors: pool bottom -> receiver (device staging on the receiver's GPU
+        // when both ends are GPUs, host staging otherwise)
         for (const auto& t : plan) {
           const int d = std::get<0>(t), rc = std::get<1>(t);
           const size_t k = std::get<2>(t);
           if (d != w) continue;
-          std::vector<uint8_t> buf(k * nb);
+          const bool on_device = staging && e->device() >= 0 && engines[rc]->device() >= 0;
           size_t got = 0;
-          guarded([&] { got = e->pop_host(buf.data(), k); });
-          buf.resize(got * nb);
-          {
+          if (on_device) {
+            guarded([&] {
+              if (dcap[rc] < k * nb) {
+                if (dbuf[rc]) staging->release(engines[rc]->device(), dbuf[rc]);
+                dbuf[rc] = nullptr;
+                dbuf[rc] = staging->alloc(engines[rc]->device(), k * nb);
+                dcap[rc] = k * nb;
+              }
+              got = e->export_device(dbuf[rc], k);
+            });
+            dcount[rc] = got;
+            ++r.device_transfers;
+          } else {
+            std::vector<uint8_t> buf(k * nb);
+            guarded([&] { got = e->pop_host(buf.data(), k); });
+            buf.resize(got * nb);
             std::lock_guard<std::mutex> lk(stage_mu);
-            staging[rc].insert(staging[rc].end(), buf.begin(), buf.end());
+            staging_host[rc].insert(staging_host[rc].end(), buf.begin(), buf.end());
           }
           r.sent += got;
           ++r.transfers_out;
         }
+        beat(w, Phase::Barrier);
         bar.wait();
-        if (!staging[w].empty()) {
-          guarded([&] { e->push_host(staging[w].data(), staging[w].size() / nb); });
-          r.received += staging[w].size() / nb;
-          ++r.transfers_in;
-          staging[w].clear();
+        beat(w, Phase::Transfer);
+        size_t in = 0;
+        if (dcount[w]) {
+          guarded([&] { e->import_device(dbuf[w], dcount[w]); });
+          in += dcount[w];
+          dcount[w] = 0;
         }
+        if (!staging_host[w].empty()) {
+          guarded([&] { e->push_host(staging_host[w].data(), staging_host[w].size() / nb); });
+          in += staging_host[w].size() / nb;
+          staging_host[w].clear();
+        }
+        if (in) {
+          r.received += in;
+          ++r.transfers_in;
+        }
+        beat(w, Phase::Barrier);
         bar.wait();
       }
       if (sizes[w] == 0) r.t_idle += secs(t0, now());
       r.t_comm += secs(t1, now());
     }
+    beat(w, Phase::Done);
     guarded([&] { r.st = e->stats(); });
   };
 
@@ -207,7 +370,13 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
   th.reserve(W);
   for (int w = 0; w < W; ++w) th.emplace_back(worker, w);
   for (auto& t : th) t.join();
+  finished = true;
+  if (watchdog.joinable()) watchdog.join();
+  if (staging)
+    for (int w = 0; w < W; ++w)
+      if (dbuf[w]) staging->release(engines[w]->device(), dbuf[w]);
   if (err) std::rethrow_exception(err);
+  rep[0].watchdog_events = watchdog_events.load();
   best = gbest;
   for (auto& r : rep) best = std::min(best, r.st.best);
   return rep;

@@ -33,6 +33,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX_HOST", "g++")
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wno-maybe-uninitialized", "-Wno-unused-function"]
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIP_LIBS = [f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
 HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
@@ -87,7 +89,8 @@ def build_cli(newest: float, jobs: int, with_hip: bool = True) -> list[Path]:
                 objs = [str(o) for o in _hip_objects(newest, jobs)]
                 app_o = OBJ / f"app_{name}.o"
                 tasks.append([[HIPCC, *HIPFLAGS, "-pthread", "-c", str(src), "-o", str(app_o)],
-                              [HIPCC, f"--offload-arch={ARCH}", "-pthread", str(app_o), *objs, "-o", str(out)]])
+                              [HIPCC, f"--offload-arch={ARCH}", "-pthread", str(app_o), *objs, *HIP_LIBS, "-o",
+                               str(out)]])
     def run_task(t):
         for c in (t if isinstance(t[0], list) else [t]):
             _run(c)
@@ -127,7 +130,8 @@ def build_hip(newest: float, jobs: int) -> Path:
         _run([HIPCC, *HIPFLAGS, "-x", "hip", *_py_includes(), "-c", str(CSRC / "bindings" / "py_hip.cpp"), "-o",
               str(bind_o)])
     if _stale(out, newest):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(bind_o), *map(str, objs), "-o", str(out)])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(bind_o), *map(str, objs), *HIP_LIBS, "-o",
+              str(out)])
     return out
 
 

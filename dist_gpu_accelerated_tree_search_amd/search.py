@@ -103,11 +103,18 @@ def solve_gpu(model, ub: int = 1, device: int = 0, m: int = 25, opts: EngineOpti
 
 def solve_workers(model, devices=(0,), cpu_threads: int = 0, ub: int = 1, m: int = 25, steal_cap: int = 250000,
                   ws: bool = True, opts: EngineOptions | None = None, engines=None, slice_min: float = 0.0005,
-                  slice_max: float = 0.05) -> SolveResult:
+                  slice_max: float = 0.05, pin: bool = False, device_steals: bool = True, watchdog_s: float = 0.0,
+                  faults: dict | None = None) -> SolveResult:
     """Several engines in ONE process — GPUs (`devices`, repeats allowed) plus an
     optional CPU worker with `cpu_threads` threads (-C 1) — driven by the native
     runner (csrc/core/runner.hpp), the analogue of ref pfsp_multigpu_cuda.c.
-    Pass `engines` to reuse engines across solves."""
+    Pass `engines` to reuse engines across solves.
+
+    pin: pin each GPU's host thread to the CPUs of the GPU's NUMA node.
+    device_steals: GPU -> GPU transfers through device staging (xGMI peer copies).
+    watchdog_s / faults: stuck-phase reporting and fault injection
+    ({"delay_us", "steal_fail_pct", "stall_worker", "stall_s", "seed"}; env
+    TTS_FAULT_* / TTS_WATCHDOG_* also apply), see csrc/core/runner.hpp."""
     gpu = len(devices) > 0
     mod = ops.require_gpu(max(devices)) if gpu else ops.cpu()
     if engines is None:
@@ -125,7 +132,8 @@ def solve_workers(model, devices=(0,), cpu_threads: int = 0, ub: int = 1, m: int
     init = [np.ascontiguousarray(nodes[round_robin_share(len(nodes), w, W)]) for w in range(W)]
     t1 = time.perf_counter()
     out = mod.run_workers(engines, init, int(best), m=m, steal_cap=steal_cap, slice_min=slice_min,
-                          slice_max=slice_max, ws=ws)
+                          slice_max=slice_max, ws=ws, pin=pin, device_steals=device_steals,
+                          watchdog_s=watchdog_s, faults=dict(faults or {}))
     t2 = time.perf_counter()
     ws_ = out["workers"]
     tree = tree1 + sum(int(w["tree"]) for w in ws_)
@@ -138,7 +146,11 @@ def solve_workers(model, devices=(0,), cpu_threads: int = 0, ub: int = 1, m: int
     return SolveResult(best=min(int(best), int(out["best"])), tree=tree, sol=sol, elapsed=t2 - t0,
                        t_init=t1 - t0, t_search=t2 - t1, workers=workers,
                        extra={"rounds": max(int(w["rounds"]) for w in ws_), "engines": engines,
-                              "sent_nodes": [int(w["sent"]) for w in ws_]})
+                              "sent_nodes": [int(w["sent"]) for w in ws_],
+                              "device_transfers": sum(int(w["device_transfers"]) for w in ws_),
+                              "dropped_transfers": sum(int(w["dropped_transfers"]) for w in ws_),
+                              "watchdog_events": int(ws_[0]["watchdog_events"]),
+                              "pinned": [bool(w["pinned"]) for w in ws_]})
 
 
 def _cpu_worker(model, mod, threads: int, opts: EngineOptions | None):

@@ -3,7 +3,11 @@
 share (begin(root) + warm_split(r, W) + run to empty) on one device and report
 max/mean over ranks. Excludes rounds and collectives (measured separately)."""
 import argparse
+import os
+import sys
 import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 import torch  # noqa: F401
 

@@ -52,3 +52,24 @@ def test_native_nqueens_gpu_cli():
     out = _cli("nqueens_gpu", "-N", "13", "-D", "1")
     assert out.returncode == 0, out.stdout + out.stderr
     assert "4674889" in out.stdout and "73712" in out.stdout
+
+
+def test_runner_device_to_device_steals_and_pinning():
+    model = PfspModel(8, 0)  # 113M nodes: long enough for steals between the engines
+    r = solve_workers(model, devices=(0, 0), m=1000, pin=True, opts=SMALL)
+    assert (r.tree, r.sol, r.best) == (113458723, 808498, 1206)
+    assert r.extra["device_transfers"] > 0
+    H = ops.hip()
+    cpus = H.device_cpus(0)
+    assert isinstance(cpus, list)
+    assert r.extra["pinned"][0] == bool(cpus and set(cpus) & set(H.allowed_cpus()))
+    # host staging path (device_steals off) gives the same tree
+    r = solve_workers(model, devices=(0, 0), m=1000, device_steals=False, opts=SMALL)
+    assert (r.tree, r.sol, r.best) == (113458723, 808498, 1206)
+    assert r.extra["device_transfers"] == 0
+
+
+def test_runner_faults_with_gpu_engines():
+    r = solve_workers(PfspModel(14, 1), devices=(0, 0, 0), m=100, opts=SMALL,
+                      faults={"delay_us": 200, "steal_fail_pct": 30})
+    assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377)

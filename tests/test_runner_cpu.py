@@ -91,3 +91,37 @@ def test_native_gpu_cli_fails_cleanly_without_device():
     out = subprocess.run([str(exe), "-i", "14", "-l", "1", "-D", "1"], capture_output=True, text=True, timeout=60)
     assert out.returncode != 0
     assert "More GPU devices requested" in out.stdout
+
+
+def test_runner_fault_injection_keeps_the_tree():
+    # random per-round delays and 50 % of planned steals dropped: same tree, and
+    # termination still happens (SURVEY §5.3 fault injection)
+    model = PfspModel(14, 0)
+    r = solve_workers(model, devices=(), engines=_cpu_engines(model, 4), m=10,
+                      faults={"delay_us": 300, "steal_fail_pct": 50, "seed": 7})
+    assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377)
+    assert r.extra["dropped_transfers"] > 0
+
+
+def test_runner_watchdog_reports_a_stalled_worker(capfd):
+    model = QueensModel(11)
+    r = solve_workers(model, devices=(), engines=_cpu_engines(model, 2), watchdog_s=0.05,
+                      faults={"stall_worker": 1, "stall_s": 0.3})
+    assert (r.tree, r.sol) == (166925, 2680)
+    assert r.extra["watchdog_events"] >= 1
+    assert "stuck in phase 'report'" in capfd.readouterr().err
+
+
+def test_runner_env_faults(monkeypatch):
+    monkeypatch.setenv("TTS_FAULT_STEAL_FAIL_PCT", "100")  # no transfer ever happens
+    model = PfspModel(14, 1)
+    r = solve_workers(model, devices=(), engines=_cpu_engines(model, 3))
+    assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377)
+    assert sum(r.extra["sent_nodes"]) == 0
+
+
+def test_cpulist_parser():
+    C = ops.cpu()
+    assert C.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert C.parse_cpulist("") == []
+    assert len(C.allowed_cpus()) >= 1
