@@ -55,18 +55,21 @@ def test_native_nqueens_gpu_cli():
 
 
 def test_runner_device_to_device_steals_and_pinning():
-    model = PfspModel(8, 0)  # 113M nodes: long enough for steals between the engines
-    r = solve_workers(model, devices=(0, 0), m=1000, pin=True, opts=SMALL)
-    assert (r.tree, r.sol, r.best) == (113458723, 808498, 1206)
-    assert r.extra["device_transfers"] > 0
+    # all initial work on engine 0: engine 1 must be fed by steals
+    model = PfspModel(8, 0)
     H = ops.hip()
+    nodes, t1, s1, best = model.warmup(model.initial_best(1), 50)
+    for dev_steals in (True, False):
+        engines = [model.make_engine("gpu", 0, SMALL) for _ in range(2)]
+        out = H.run_workers(engines, [nodes, nodes[:0]], int(best), m=1000, pin=True, device_steals=dev_steals)
+        ws = out["workers"]
+        assert (t1 + sum(w["tree"] for w in ws), s1 + sum(w["sol"] for w in ws), out["best"]) == \
+            (113458723, 808498, 1206)
+        assert ws[1]["received"] > 0
+        assert (ws[0]["device_transfers"] > 0) == dev_steals
     cpus = H.device_cpus(0)
     assert isinstance(cpus, list)
-    assert r.extra["pinned"][0] == bool(cpus and set(cpus) & set(H.allowed_cpus()))
-    # host staging path (device_steals off) gives the same tree
-    r = solve_workers(model, devices=(0, 0), m=1000, device_steals=False, opts=SMALL)
-    assert (r.tree, r.sol, r.best) == (113458723, 808498, 1206)
-    assert r.extra["device_transfers"] == 0
+    assert ws[0]["pinned"] == bool(cpus and set(cpus) & set(H.allowed_cpus()))
 
 
 def test_runner_faults_with_gpu_engines():
