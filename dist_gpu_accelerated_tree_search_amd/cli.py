@@ -7,8 +7,10 @@ pfsp:  -D 0            CPU only: -C threads (0/1 = sequential, ref pfsp_c / pfsp
        -D 1            one GPU (ref pfsp_multigpu_cuda.out -D 1)
        -D N            N GPUs, one process per GPU (ranks spawned here, or run the
                        same command under torchrun); -w / -L enable work sharing
-                       inside a node / across nodes (ref -w, -L); -C 1 adds CPU
-                       workers on each rank (ref -C).
+                       inside a node / across nodes (ref -w, -L).
+       -C 1 (D >= 1)   add a CPU worker next to the GPUs (ref -C 1); runs the
+                       single-process native runner (one host thread per GPU,
+                       xGMI peer steals), as does --single-process.
 nqueens: -D 0 CPU sequential (ref nqueens_c), -D >= 1 GPU(s).
 Results: the reference's stdout blocks, plus a CSV row (singlegpu.csv,
 multigpu.csv or dist_multigpu.csv) and optionally a JSON record (--json).
@@ -40,6 +42,13 @@ def _pfsp_parser() -> argparse.ArgumentParser:
     ap.add_argument("-L", "--L", type=int, default=1)
     ap.add_argument("-p", "--perc", type=int, default=50)
     ap.add_argument("--max-parents", type=int, default=1 << 18)
+    ap.add_argument("--single-process", action="store_true",
+                    help="all GPUs driven by one process (native runner) instead of one process per GPU")
+    ap.add_argument("--gpus-list", default=None, help="comma-separated device ids (single-process mode)")
+    ap.add_argument("--steal-cap", type=int, default=None, help="max nodes per transfer (default 5*M)")
+    ap.add_argument("--comm-period", type=float, default=0.5,
+                    help="minimum local search between coordination rounds, ms (adaptive up to 50 ms)")
+    ap.add_argument("--pin", type=int, default=1, help="pin GPU host threads to the GPU's NUMA node")
     ap.add_argument("--ring-gb", type=float, default=16.0)
     ap.add_argument("--json", default=None, help="append a JSON run record to this file")
     ap.add_argument("--csv-dir", default=".", help="directory of the CSV statistics files")
@@ -68,6 +77,9 @@ def _validate_pfsp(a) -> None:
         fail("Error: unsupported number of GPU(s)")
     if a.C < 0:
         fail("Error: unsupported number of CPU Core(s)")
+    if a.D >= 1 and a.C > 1:
+        fail("C is set to %d. Invalid option for this version.\nChoose 0 to unable and 1 to enable multi-core. "
+             "Mapping automatically done." % a.C)
     if a.ws not in (0, 1):
         fail("Error: unsupported Intra-node Work Stealing option")
     if a.L not in (0, 1):
@@ -76,10 +88,54 @@ def _validate_pfsp(a) -> None:
         fail("Error: unsupported WS percentage for popFrontBulkFree")
 
 
+def _steal_cap(a) -> int:
+    return a.steal_cap if a.steal_cap else 5 * a.M
+
+
 def _rank_spec(a) -> dict:
     return {"problem": "pfsp", "inst": a.inst, "lb": a.lb, "ub": a.ub, "backend": "gpu",
             "engine": {"max_parents": a.max_parents, "ring_bytes": int(a.ring_gb * (1 << 30))},
-            "dist": {"m": a.m, "init_per_rank": a.m, "steal_cap": 5 * a.M, "ws": bool(a.ws), "L": bool(a.L)}}
+            "dist": {"m": a.m, "init_per_rank": a.m, "steal_cap": _steal_cap(a), "ws": bool(a.ws), "L": bool(a.L),
+                     "slice_min_s": a.comm_period * 1e-3}, "pin": bool(a.pin)}
+
+
+def _cpu_worker_threads(n_gpus: int) -> int:
+    """ref pfsp_multigpu_cuda.c:61-69: nprocs/deviceCount threads per GPU, one of which
+    drives the GPU; here the CPU threads of all GPUs form one multithreaded worker."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, n - n_gpus)
+
+
+def _pfsp_single_process(a, model) -> int:
+    from .models.pfsp import EngineOptions
+    from .ops import gpu_count
+    from .search import solve_workers
+
+    devices = [int(x) for x in a.gpus_list.split(",")] if a.gpus_list else list(range(a.D))
+    if len(devices) != a.D and a.gpus_list:
+        a.D = len(devices)
+    if devices and max(devices) >= gpu_count():
+        print("Execution Terminated. More GPU devices requested than the ones available")
+        return 1
+    threads = _cpu_worker_threads(len(devices)) if a.C == 1 else 0
+    print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, a.D, a.C, a.ws, 1, a.L, 2))
+    opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * 2**30), cpu_batch=a.T,
+                         cpu_threads=max(1, threads))
+    r = solve_workers(model, devices=tuple(devices), cpu_threads=threads, ub=a.ub, m=a.m, steal_cap=_steal_cap(a),
+                      ws=bool(a.ws), opts=opts, slice_min=a.comm_period * 1e-3, pin=bool(a.pin))
+    print(report.phase("Initial search on CPU completed", 0, 0, r.t_init))
+    print(report.phase("Search on Parallel GPU completed", r.tree, r.sol, r.t_search))
+    print("\nExploration terminated.")
+    print(report.pfsp_results(r.best, r.tree, r.sol, r.elapsed))
+    if not a.no_csv:
+        report.write_multi_gpu_csv(os.path.join(a.csv_dir, "multigpu.csv"), a.inst, a.lb, len(devices),
+                                   1 if threads else 0, a.ws, r.best, a.m, a.M, a.T, r.elapsed, r.tree, r.sol,
+                                   r.workers)
+    _json(a, model, r, len(devices))
+    return 0
 
 
 def pfsp_main(argv: list[str]) -> int:
@@ -103,6 +159,9 @@ def pfsp_main(argv: list[str]) -> int:
                                        a.m, a.M, a.T, r.elapsed, r.tree, r.sol, r.workers)
         _json(a, model, r, 0)
         return 0
+
+    if world_env == 1 and (a.C == 1 or a.single_process or a.gpus_list):
+        return _pfsp_single_process(a, model)
 
     if a.D == 1 and world_env == 1:
         print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, 1, a.C, a.ws, 1, a.L, 2))

@@ -27,7 +27,9 @@ import numpy as np
 
 from ..search import SolveResult
 from ..utils.report import WorkerStats
+from . import checkpoint as ckpt
 from .comm import Comm, plan_sharing
+from .faults import Faults, Watchdog
 
 
 @dataclass
@@ -45,6 +47,17 @@ class DistConfig:
     engine_warmup: bool = True
     warm_window: int = 2048
     warm_passes: int = 1
+    # checkpoint / resume (parallel/checkpoint.py): snapshot every
+    # `checkpoint_every` rounds and when `max_rounds` stops the solve early
+    checkpoint_dir: str | None = None
+    checkpoint_every: int = 0
+    max_rounds: int = 0
+    resume: bool = False
+    # failure detection / fault injection (parallel/faults.py; env TTS_FAULT_*)
+    watchdog_s: float = 0.0
+    watchdog_abort: bool = False
+    fault_delay_us: int | None = None
+    fault_steal_fail_pct: int | None = None
     verbose: bool = False
 
 
@@ -83,6 +96,14 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
 
     # ---- Step 1: redundant, deterministic warm-up on every rank ----
     best = model.initial_best(ub)
+    if cfg.resume:
+        if not cfg.checkpoint_dir:
+            raise ValueError("resume needs checkpoint_dir")
+        nodes, tree0, sol0, best0, rounds0 = ckpt.load_all(cfg.checkpoint_dir, model)
+        best = min(int(best), best0)
+        engine.begin(np.ascontiguousarray(nodes[rank::world]), int(best))
+        rs.t_init = time.perf_counter() - t_start
+        return _rounds(model, engine, comm, cfg, rs, t_start, best, tree0, sol0)
     if world > 1 and cfg.engine_warmup:
         # on the engine: wide frontier in a few device iterations, strided share
         tree1 = sol1 = 0
@@ -93,7 +114,7 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
     nodes, tree1, sol1, best = model.warmup(best, world * cfg.init_per_rank)
     mine = np.ascontiguousarray(nodes[round_robin_share(len(nodes), rank, world)])
     rs.t_init = time.perf_counter() - t_start
-    if world == 1:  # one fused native solve, no rounds
+    if world == 1 and not cfg.max_rounds and not cfg.checkpoint_dir:  # one fused native solve, no rounds
         st = engine.solve(mine, int(best))
         elapsed = time.perf_counter() - t_start
         w = WorkerStats(tree=int(st["tree"]), sol=int(st["sol"]), gen_child=int(st["tree"]),
@@ -115,6 +136,9 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, rs: RankStats, t_start: 
     share = cfg.ws or cfg.L
     node_of = lambda r: r // max(1, comm.topo.local_world)  # noqa: E731
     slice_s = cfg.slice_min_s
+    faults = Faults(rank, cfg.fault_delay_us, cfg.fault_steal_fail_pct)
+    dog = Watchdog(cfg.watchdog_s, cfg.watchdog_abort)
+    complete = True
     t_loop = time.perf_counter()
     while True:
         t0 = time.perf_counter()
@@ -122,7 +146,10 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, rs: RankStats, t_start: 
         t1 = time.perf_counter()
         rs.t_run += t1 - t0
         size = engine.size()
+        faults.before_round()
+        dog.arm(f"rank {rank}/{world} round {rs.rounds + 1} pool {size} best {engine.best}")
         st = comm.allgather_i64([size, engine.best])
+        dog.disarm()
         rs.rounds += 1
         gbest = int(st[:, 1].min())
         if gbest < engine.best:
@@ -134,6 +161,7 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, rs: RankStats, t_start: 
         starving = bool((sizes < cfg.m).any())
         if share and world > 1 and starving:
             plan = plan_sharing(sizes, cfg.m, cfg.steal_cap, node_of, intra=cfg.ws, inter=cfg.L)
+            plan = faults.filter_plan(plan, rs.rounds)
             if plan:
                 sent, got = comm.execute_transfers(plan, engine, model.node_bytes)
                 rs.sent += sent
@@ -146,6 +174,16 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, rs: RankStats, t_start: 
         if size == 0:
             rs.t_idle += time.perf_counter() - t0
         rs.t_comm += time.perf_counter() - t1
+        stop = cfg.max_rounds > 0 and rs.rounds >= cfg.max_rounds
+        if cfg.checkpoint_dir and (stop or (cfg.checkpoint_every > 0 and rs.rounds % cfg.checkpoint_every == 0)):
+            est = engine.stats()
+            ckpt.save(cfg.checkpoint_dir, rank, world, model, engine,
+                      int(est["tree"]) + (tree1 if rank == 0 else 0), int(est["sol"]) + (sol1 if rank == 0 else 0),
+                      min(int(est["best"]), int(gbest)), rs.rounds)
+            comm.barrier()  # every file is complete before anyone may resume from it
+        if stop:
+            complete = False
+            break
     t_search = time.perf_counter() - t_loop
 
     # ---- Step 3 (nothing left by construction) + reductions ----
@@ -166,4 +204,5 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, rs: RankStats, t_start: 
     return SolveResult(best=gbest, tree=int(tot[0]), sol=int(tot[1]), elapsed=elapsed, t_init=rs.t_init,
                        t_search=t_search, t_tail=0.0, workers=workers,
                        extra={"rounds": rs.rounds, "sent_nodes": [int(r[2]) for r in per],
-                              "received_nodes": [int(r[3]) for r in per], "world": world})
+                              "received_nodes": [int(r[3]) for r in per], "world": world, "complete": complete,
+                              "dropped_transfers": faults.dropped, "watchdog_events": dog.events})

@@ -27,6 +27,10 @@ def solve_rank(spec: dict) -> dict:
         model = build_model(spec)
         opts = EngineOptions(**spec.get("engine", {}))
         device = int(spec.get("device", comm.topo.local_rank)) if backend == "gpu" else 0
+        if backend == "gpu" and spec.get("pin", False):
+            from .topology import pin_to_device
+
+            pin_to_device(device)
         engine = model.make_engine(backend, device, opts)
         cfg = DistConfig(**spec.get("dist", {}))
         res = None

@@ -107,3 +107,45 @@ def test_repeated_solves_reuse_engine():
     spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu", "repeat": 3}
     res = spawn_local(2, solve_rank, (spec,), timeout=300)
     assert (res[1]["tree"], res[1]["sol"], res[1]["best"]) == GOLD
+
+
+def test_checkpoint_and_resume_on_a_different_world(tmp_path):
+    d = str(tmp_path / "ckpt")
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu",
+            "dist": {"max_rounds": 4, "checkpoint_dir": d, "slice_min_s": 0.0002, "slice_max_s": 0.0005}}
+    res = spawn_local(2, solve_rank, (spec,), timeout=300)
+    assert res[0]["extra"]["complete"] is False
+    assert res[0]["tree"] < GOLD[0]
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu", "dist": {"resume": True, "checkpoint_dir": d}}
+    res = spawn_local(3, solve_rank, (spec,), timeout=300)
+    assert res[0]["extra"]["complete"] is True
+    assert (res[0]["tree"], res[0]["sol"], res[0]["best"]) == GOLD
+
+
+def test_checkpoint_rejects_another_model(tmp_path):
+    from dist_gpu_accelerated_tree_search_amd import PfspModel
+    from dist_gpu_accelerated_tree_search_amd.parallel import checkpoint
+
+    d = str(tmp_path / "c")
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu", "dist": {"max_rounds": 1, "checkpoint_dir": d}}
+    spawn_local(2, solve_rank, (spec,), timeout=300)
+    nodes, tree, sol, best, rounds = checkpoint.load_all(d, PfspModel(14, 0))
+    assert rounds == 1 and best == 1377 and tree > 0
+    with pytest.raises(ValueError):
+        checkpoint.load_all(d, PfspModel(13, 0))
+
+
+def test_fault_injection_keeps_the_tree():
+    spec = {"problem": "pfsp", "inst": 14, "lb": 1, "backend": "cpu",
+            "dist": {"fault_delay_us": 300, "fault_steal_fail_pct": 50, "m": 50}}
+    res = spawn_local(3, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == GOLD
+
+
+def test_watchdog_reports_a_slow_round():
+    spec = {"problem": "nqueens", "N": 9, "backend": "cpu",
+            "dist": {"watchdog_s": 0.02, "fault_delay_us": 150_000, "slice_min_s": 0.0001}}
+    res = spawn_local(2, solve_rank, (spec,), timeout=300)
+    assert (res[0]["tree"], res[0]["sol"]) == (8393, 352)
+    assert sum(r["extra"]["watchdog_events"] for r in res) >= 1
