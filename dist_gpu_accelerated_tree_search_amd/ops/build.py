@@ -135,6 +135,27 @@ def build_hip(newest: float, jobs: int) -> Path:
     return out
 
 
+SANITIZERS = {"tsan": ["-fsanitize=thread"], "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]}
+
+
+def build_sanitized_selftests(kinds=("tsan", "asan"), jobs: int = 2) -> dict[str, Path]:
+    """Host runtime self-test (csrc/tests/runtime_selftest.cpp) under TSan and
+    ASan+UBSan. Host code only: GPU sanitizers are not used."""
+    BIN.mkdir(parents=True, exist_ok=True)
+    src = CSRC / "tests" / "runtime_selftest.cpp"
+    newest = _sources_mtime()
+    tasks, outs = [], {}
+    for k in kinds:
+        out = BIN / f"runtime_selftest_{k}"
+        outs[k] = out
+        if _stale(out, newest):
+            tasks.append([CXX, "-O1", "-g", "-std=c++17", "-pthread", *SANITIZERS[k], f"-I{CSRC}", str(src), "-o",
+                          str(out)])
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(_run, tasks))
+    return outs
+
+
 def build_all(only: str | None = None, jobs: int | None = None) -> dict[str, Path]:
     jobs = jobs or min(16, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))
     newest = _sources_mtime()
