@@ -202,6 +202,10 @@ def pfsp_main(argv: list[str]) -> int:
     if not a.no_csv:
         report.write_multi_gpu_csv(os.path.join(a.csv_dir, "multigpu.csv"), a.inst, a.lb, D, 0, a.ws, res["best"],
                                    a.m, a.M, a.T, res["elapsed"], res["tree"], res["sol"], workers)
+        # one process per GPU = the reference's distributed driver layout (one GPU per rank)
+        report.write_dist_multi_gpu_csv(os.path.join(a.csv_dir, "dist_multigpu.csv"), a.inst, a.lb, 1, 0, a.L, D,
+                                        res["best"], a.m, a.M, a.T, res["elapsed"], res["tree"], res["sol"], workers,
+                                        [w.steals for w in workers], [w.t_pool_ops for w in workers])
     if a.json:
         report.write_json_record(a.json, {**model.describe(), "n_gpus": D, "tree": res["tree"], "sol": res["sol"],
                                            "best": res["best"], "elapsed": res["elapsed"],

@@ -76,3 +76,15 @@ def test_runner_faults_with_gpu_engines():
     r = solve_workers(PfspModel(14, 1), devices=(0, 0, 0), m=100, opts=SMALL,
                       faults={"delay_us": 200, "steal_fail_pct": 30})
     assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377)
+
+
+def test_python_cli_cpu_worker_and_single_process(tmp_path):
+    import sys
+
+    base = [sys.executable, "-m", "dist_gpu_accelerated_tree_search_amd", "pfsp", "-i", "14", "-l", "1",
+            "--csv-dir", str(tmp_path), "--ring-gb", "1"]
+    for extra in (["-D", "1", "-C", "1"], ["-D", "2", "--single-process", "--gpus-list", "0,0"]):
+        out = subprocess.run(base + extra, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert "2573652" in out.stdout and "1377" in out.stdout
+    assert (tmp_path / "multigpu.csv").exists()
