@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""BASELINE.json configurations beyond the headline (bench.py):
+
+  queens14_cpu   N-Queens N=14 sequential CPU (ref nqueens_c.out: 2.24 s, 12.2 M nodes/s here)
+  queens17_gpu   N-Queens N=17 g=1 on one GPU (ref sequential 807 s)
+  ta014_lb1      PFSP ta014 LB1 on one GPU (headline instance)
+  ta021_lb1d     PFSP ta021 (20x20) LB1_d on --gpus GPUs (ref V100 CUDA 1308.79 s, MI50 HIP 2538.23 s,
+                 ChplBB 1 LUMI node 6600.81 s; bound not recorded by the reference)
+  ta056_lb2      PFSP ta056 (50x20) LB2 on --gpus GPUs (no reference number)
+
+Each config runs in its own process under a time limit and prints one JSON line
+(tree, sol, best, seconds, nodes/s, reference seconds when known). Several GPUs are
+driven by the single-process native runner (one host thread per GPU, xGMI steals).
+
+    python bench/suite.py [--gpus N] [--only name,...] [--limit SECONDS]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CONFIGS = {
+    "queens14_cpu": {"problem": "queens", "N": 14, "backend": "cpu", "ref_s": 2.24,
+                     "gold": (27358552, 365596)},
+    "queens17_gpu": {"problem": "queens", "N": 17, "backend": "gpu", "ref_s": 807.0,
+                     "gold": (8017021931, 95815104)},
+    "ta014_lb1": {"problem": "pfsp", "inst": 14, "lb": 1, "backend": "gpu", "gold": (2573652, 2648, 1377)},
+    "ta021_lb1d": {"problem": "pfsp", "inst": 21, "lb": 0, "backend": "gpu", "multi": True, "ref_s": 1308.79},
+    "ta056_lb2": {"problem": "pfsp", "inst": 56, "lb": 2, "backend": "gpu", "multi": True},
+}
+
+
+def run_one(name: str, gpus: int) -> dict:
+    sys.path.insert(0, ROOT)
+    import torch  # noqa: F401
+
+    from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel, QueensModel
+    from dist_gpu_accelerated_tree_search_amd.search import solve_cpu, solve_gpu, solve_workers
+
+    c = CONFIGS[name]
+    model = QueensModel(c["N"]) if c["problem"] == "queens" else PfspModel(c["inst"], c["lb"])
+    t0 = time.perf_counter()
+    if c["backend"] == "cpu":
+        r = solve_cpu(model)
+        n = 0
+    elif c.get("multi") and gpus > 1:
+        r = solve_workers(model, devices=tuple(range(gpus)), opts=EngineOptions(ring_bytes=64 << 30), pin=True)
+        n = gpus
+    else:
+        opts = EngineOptions(max_parents=1 << 20, ring_bytes=64 << 30) if c["problem"] == "queens" else \
+            EngineOptions(ring_bytes=64 << 30)
+        r = solve_gpu(model, opts=opts)
+        n = 1
+    dt = time.perf_counter() - t0
+    rec = {"config": name, "n_gpus": n, "tree": r.tree, "sol": r.sol, "best": r.best, "seconds": dt,
+           "nodes_per_s": r.tree / dt}
+    if "gold" in c:
+        rec["golden_ok"] = tuple(list((r.tree, r.sol, r.best))[:len(c["gold"])]) == c["gold"]
+    if "ref_s" in c:
+        rec["ref_seconds"] = c["ref_s"]
+        rec["speedup_vs_ref"] = c["ref_s"] / dt
+    return rec
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--limit", type=float, default=600.0, help="seconds per config")
+    ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
+    a = ap.parse_args()
+    if a.child:
+        print(json.dumps(run_one(a.child, a.gpus)), flush=True)
+        return 0
+    names = a.only.split(",") if a.only else list(CONFIGS)
+    for name in names:
+        try:
+            out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", name, "--gpus", str(a.gpus)],
+                                 capture_output=True, text=True, timeout=a.limit)
+            lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+            if out.returncode != 0 or not lines:
+                print(json.dumps({"config": name, "error": (out.stderr or out.stdout)[-500:]}), flush=True)
+            else:
+                print(lines[-1], flush=True)
+        except subprocess.TimeoutExpired:
+            print(json.dumps({"config": name, "timeout_s": a.limit}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
