@@ -13,4 +13,4 @@ __version__ = "0.1.0"
 
 from .models.nqueens import QueensModel  # noqa: E402,F401
 from .models.pfsp import EngineOptions, PfspModel  # noqa: E402,F401
-from .search import SolveResult, solve_cpu, solve_engine, solve_gpu  # noqa: E402,F401
+from .search import SolveResult, solve_cpu, solve_engine, solve_gpu, solve_workers  # noqa: E402,F401
