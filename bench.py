@@ -40,11 +40,14 @@ def main() -> int:
     ap.add_argument("--inst", type=int, default=14)
     ap.add_argument("--lb", type=int, default=1)
     ap.add_argument("--ub", type=int, default=1)
-    ap.add_argument("--max-parents", type=int, default=1 << 18)
+    ap.add_argument("--max-parents", type=int, default=1 << 19)
     ap.add_argument("--ring-gb", type=float, default=8.0)
     ap.add_argument("--init-per-rank", type=int, default=25)
     ap.add_argument("--no-ws", action="store_true", help="static partition (ref -w 0 / -L 0)")
     ap.add_argument("--backend", choices=["gpu", "cpu"], default="gpu")
+    ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
+                    help="process group for node transfers (gloo: ranks may share one GPU, for tests)")
+    ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default LOCAL_RANK)")
     a = ap.parse_args()
 
     import torch  # noqa: F401  (before the HIP extension: one HIP runtime per process)
@@ -56,10 +59,11 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    comm = Comm(use_gpu=(a.backend == "gpu"))
+    comm = Comm(use_gpu=(a.backend == "gpu" and a.comm == "nccl"))
     model = PfspModel(a.inst, a.lb)
     opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * (1 << 30)))
-    engine = model.make_engine(a.backend, comm.topo.local_rank if a.backend == "gpu" else 0, opts)
+    device = (comm.topo.local_rank if a.device is None else a.device) if a.backend == "gpu" else 0
+    engine = model.make_engine(a.backend, device, opts)
     cfg = DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws)
     golden = GOLDEN.get((a.inst, a.lb)) if a.ub == 1 else None
 
@@ -83,6 +87,11 @@ def main() -> int:
     dt = float(comm.allgather_f64([dt_local]).max())
     value = tree / dt
     if comm.rank == 0:
+        ex = last.extra
+        log(f"last step: elapsed {last.elapsed * 1e3:.3f} ms, init {last.t_init * 1e3:.3f} ms, "
+            f"search {last.t_search * 1e3:.3f} ms, rounds {ex.get('rounds')}, "
+            f"per-rank tree {[w.tree for w in last.workers]}, control plane "
+            f"{'shm' if getattr(comm, 'ctl', None) is not None else comm.backend}")
         rec = {
             "metric": "tree-nodes/sec (whole node), PFSP ta014 LB1 at 1/2/4/8 MI355X",
             "value": value,

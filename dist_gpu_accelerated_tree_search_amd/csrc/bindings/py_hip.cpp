@@ -23,7 +23,7 @@ namespace {
 using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 
 EngineConfig make_cfg(int device, size_t max_parents, size_t ring_bytes, int iters_small, int iters_large,
-                      bool use_graphs, uintptr_t stream) {
+                      bool use_graphs, uintptr_t stream, int iters_first) {
   EngineConfig c;
   c.device = device;
   c.max_parents = max_parents;
@@ -32,6 +32,7 @@ EngineConfig make_cfg(int device, size_t max_parents, size_t ring_bytes, int ite
   c.iters_large = iters_large;
   c.use_graphs = use_graphs;
   c.external_stream = stream;
+  c.iters_first = iters_first;
   return c;
 }
 
@@ -89,27 +90,29 @@ PYBIND11_MODULE(_tts_hip, m) {
   m.def(
       "make_pfsp_engine",
       [](int jobs, int machines, std::vector<int> p, int lb, int device, size_t max_parents, size_t ring_bytes,
-         int iters_small, int iters_large, bool use_graphs, uintptr_t stream, int taillard_id) {
+         int iters_small, int iters_large, bool use_graphs, uintptr_t stream, int taillard_id, int iters_first) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p), taillard_id);
         py::gil_scoped_release nogil;
         return make_pfsp_engine(in, lb,
-                                make_cfg(device, max_parents, ring_bytes, iters_small, iters_large, use_graphs, stream));
+                                make_cfg(device, max_parents, ring_bytes, iters_small, iters_large, use_graphs, stream,
+                                         iters_first));
       },
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("device") = 0,
       py::arg("max_parents") = size_t(1) << 18, py::arg("ring_bytes") = size_t(16) << 30, py::arg("iters_small") = 6,
-      py::arg("iters_large") = 48, py::arg("use_graphs") = true, py::arg("stream") = 0, py::arg("taillard_id") = 0);
+      py::arg("iters_large") = 48, py::arg("use_graphs") = true, py::arg("stream") = 0, py::arg("taillard_id") = 0,
+      py::arg("iters_first") = 24);
 
   m.def(
       "make_queens_engine",
       [](int N, int G, int device, size_t max_parents, size_t ring_bytes, int iters_small, int iters_large,
-         bool use_graphs, uintptr_t stream) {
+         bool use_graphs, uintptr_t stream, int iters_first) {
         py::gil_scoped_release nogil;
         return make_queens_engine(
-            N, G, make_cfg(device, max_parents, ring_bytes, iters_small, iters_large, use_graphs, stream));
+            N, G, make_cfg(device, max_parents, ring_bytes, iters_small, iters_large, use_graphs, stream, iters_first));
       },
       py::arg("N"), py::arg("G") = 1, py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 20,
       py::arg("ring_bytes") = size_t(16) << 30, py::arg("iters_small") = 6, py::arg("iters_large") = 48,
-      py::arg("use_graphs") = true, py::arg("stream") = 0);
+      py::arg("use_graphs") = true, py::arg("stream") = 0, py::arg("iters_first") = 24);
 
   m.def(
       "pfsp_bounds",

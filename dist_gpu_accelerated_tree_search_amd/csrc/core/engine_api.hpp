@@ -14,6 +14,7 @@ struct EngineConfig {
   size_t ring_bytes = size_t(16) << 30;  // device ring capacity in bytes (rounded down to 2^k nodes)
   int iters_small = 6;                   // iterations per small graph (multiple of 6)
   int iters_large = 48;                  // iterations per large graph (multiple of 6)
+  int iters_first = 24;                  // first replay after begin(): covers a small tree in one graph
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };

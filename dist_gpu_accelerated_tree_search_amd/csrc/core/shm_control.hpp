@@ -1,0 +1,173 @@
+// Intra-node control plane for the one-process-per-GPU runtime: the small status
+// exchanges of every round (pool size, incumbent, termination, final counters)
+// go through a POSIX shared-memory segment instead of RCCL collectives.
+//
+// Why: a round's record is a few int64 per rank. Over RCCL each exchange is a
+// host->device copy, a collective kernel and a device->host copy with a stream
+// sync (tens of microseconds); ta014 LB1 solves in ~0.4 ms on one MI355X, so
+// two such collectives per solve would eat most of the gain of a second GPU.
+// Through shared memory an all-gather is one cache-line store per rank and a
+// spin on the others' lines (~1 us). Node payloads still move GPU -> GPU over
+// xGMI (RCCL send/recv, parallel/comm.py).
+//
+// Parity: the reference's intra-node coordination is also shared memory — C11
+// atomics and spin locks between OpenMP threads (ref pfsp_multigpu_cuda.c:30-50
+// checkBest, common/util.c:4-38 allIdle); its inter-node rounds are MPI
+// Allreduce/Allgather (ref pfsp_dist_multigpu_cuda.c:364-469). Here processes
+// replace threads, the segment replaces the shared address space, and the
+// all-gather has collective semantics (every rank calls it in the same order).
+//
+// Protocol: slot[parity][rank] = {seq, values}. Round r writes parity r&1, then
+// publishes seq = r (release) and waits until every rank's seq reaches r
+// (acquire). A rank can only write parity r&1 again at round r+2, which needs
+// every rank to have posted round r+1, i.e. to have finished reading round r —
+// so two buffers are enough and no reset is ever needed. A rank that does not
+// arrive within the timeout raises (failure detection).
+#pragma once
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+namespace tts {
+
+class ShmControl {
+ public:
+  static constexpr int kMaxVals = 15;
+  static constexpr uint64_t kMagic = 0x7474735f63746c31ull;  // "tts_ctl1"
+
+  // create=true: make (or replace) the segment `name` (rank 0); otherwise open it.
+  ShmControl(const std::string& name, int rank, int world, bool create) : name_(name), rank_(rank), world_(world) {
+    if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("ShmControl: bad rank/world");
+    if (name.empty() || name[0] != '/') throw std::invalid_argument("ShmControl: name must start with '/'");
+    bytes_ = sizeof(Header) + 2 * static_cast<size_t>(world) * sizeof(Slot);
+    int fd = -1;
+    if (create) {
+      (void)shm_unlink(name.c_str());  // stale segment of a crashed run
+      fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0) throw std::runtime_error("shm_open(create " + name + "): " + std::strerror(errno));
+      if (ftruncate(fd, static_cast<off_t>(bytes_)) != 0) {
+        const int e = errno;
+        close(fd);
+        (void)shm_unlink(name.c_str());
+        throw std::runtime_error(std::string("ftruncate: ") + std::strerror(e));
+      }
+    } else {
+      fd = shm_open(name.c_str(), O_RDWR, 0600);
+      if (fd < 0) throw std::runtime_error("shm_open(" + name + "): " + std::strerror(errno));
+      struct stat sb;
+      if (fstat(fd, &sb) != 0 || static_cast<size_t>(sb.st_size) < bytes_) {
+        close(fd);
+        throw std::runtime_error("ShmControl: segment " + name + " has the wrong size (world mismatch?)");
+      }
+    }
+    void* p = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) throw std::runtime_error(std::string("mmap: ") + std::strerror(errno));
+    base_ = static_cast<char*>(p);
+    hdr_ = reinterpret_cast<Header*>(base_);
+    slots_ = reinterpret_cast<Slot*>(base_ + sizeof(Header));
+    if (create) {
+      std::memset(base_, 0, bytes_);  // ftruncate already zeroes; be explicit
+      hdr_->world = world;
+      hdr_->best.store(INT64_MAX, std::memory_order_relaxed);
+      std::atomic_thread_fence(std::memory_order_release);
+      hdr_->magic.store(kMagic, std::memory_order_release);
+    } else {
+      if (hdr_->magic.load(std::memory_order_acquire) != kMagic || hdr_->world != world) {
+        munmap(base_, bytes_);
+        throw std::runtime_error("ShmControl: segment " + name + " is not initialised for this world size");
+      }
+    }
+  }
+
+  ~ShmControl() {
+    if (base_) munmap(base_, bytes_);
+  }
+  ShmControl(const ShmControl&) = delete;
+  ShmControl& operator=(const ShmControl&) = delete;
+
+  // Remove the name once every rank has mapped the segment (the mapping stays valid).
+  void unlink() { (void)shm_unlink(name_.c_str()); }
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  uint64_t rounds() const { return round_; }
+
+  // out[r * n + i] = value i of rank r. Collective: every rank calls it in the same order.
+  void allgather(const int64_t* vals, int n, int64_t* out, double timeout_s) {
+    if (n < 0 || n > kMaxVals) throw std::invalid_argument("ShmControl::allgather: at most 15 values");
+    const uint64_t r = ++round_;
+    const int par = static_cast<int>(r & 1);
+    Slot& mine = slot(par, rank_);
+    for (int i = 0; i < n; ++i) mine.v[i] = vals[i];
+    mine.seq.store(r, std::memory_order_release);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int q = 0; q < world_; ++q) {
+      Slot& s = slot(par, q);
+      unsigned spins = 0;
+      while (s.seq.load(std::memory_order_acquire) < r) {
+        if (++spins < 2048) {
+          __builtin_ia32_pause();
+          continue;
+        }
+        std::this_thread::yield();
+        if ((spins & 255) == 0 && timeout_s > 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+          throw std::runtime_error("ShmControl: rank " + std::to_string(q) + " did not reach round " +
+                                   std::to_string(r) + " within " + std::to_string(timeout_s) + " s");
+      }
+      for (int i = 0; i < n; ++i) out[q * n + i] = s.v[i];
+    }
+  }
+
+  void barrier(double timeout_s) {
+    int64_t dummy = 0;
+    allgather(&dummy, 0, &dummy, timeout_s);
+  }
+
+  // Node-wide incumbent: atomic MIN visible to every rank at once (checkBest).
+  int64_t offer_best(int64_t b) {
+    int64_t cur = hdr_->best.load(std::memory_order_relaxed);
+    while (b < cur && !hdr_->best.compare_exchange_weak(cur, b, std::memory_order_acq_rel)) {
+    }
+    return b < cur ? b : cur;
+  }
+  int64_t best() const { return hdr_->best.load(std::memory_order_acquire); }
+
+ private:
+  struct alignas(128) Header {
+    std::atomic<uint64_t> magic;
+    int world;
+    int pad;
+    std::atomic<int64_t> best;
+  };
+  struct alignas(128) Slot {
+    std::atomic<uint64_t> seq;
+    int64_t v[kMaxVals];
+  };
+  static_assert(sizeof(Slot) == 128, "one cache-line pair per slot");
+  static_assert(std::atomic<uint64_t>::is_always_lock_free, "lock-free atomics needed across processes");
+
+  Slot& slot(int par, int r) { return slots_[par * world_ + r]; }
+
+  std::string name_;
+  int rank_, world_;
+  size_t bytes_ = 0;
+  char* base_ = nullptr;
+  Header* hdr_ = nullptr;
+  Slot* slots_ = nullptr;
+  uint64_t round_ = 0;
+};
+
+}  // namespace tts

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -95,6 +96,17 @@ class DeviceEngine final : public IEngine {
     const int per_cu = std::max(1, Traits::blocks_per_cu());
     grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, static_cast<size_t>(cus) * per_cu)));
     upload_ctl();
+    // Pipelined replays: queue the next graph while one runs when the last known
+    // pool spans a whole parent window (spec_min_). Queuing it earlier
+    // (TTS_SPECULATE=1) was measured slower on ta014: an empty iteration still
+    // costs ~4.5 us and two queued graphs are still ~13 us apart
+    // (profiles/r1f).
+    {
+      const char* e = std::getenv("TTS_SPECULATE");
+      spec_min_ = (e && e[0] == '1') ? 1 : cfg_.max_parents;
+      const char* p = std::getenv("TTS_POLL");
+      poll_ = !(p && p[0] == '0');
+    }
     // graphs of 6, 12, 24, ... iterations up to iters_large; run() picks one from
     // the pool size and the worst-case ring growth
     for (int k = cfg_.iters_small; k <= cfg_.iters_large; k *= 2) {
@@ -241,7 +253,7 @@ class DeviceEngine final : public IEngine {
       size_t inflight_growth = static_cast<size_t>(ks_[gi] + 1) * buf_nodes_;
       while (!inflight_.empty()) {
         const bool budget_ok = (max_launches < 0 || launches < max_launches) && (max_seconds <= 0 || elapsed() < max_seconds);
-        if (inflight_.size() == 1 && budget_ok && known >= cfg_.max_parents) {
+        if (inflight_.size() == 1 && budget_ok && known >= spec_min_) {
           const int g2 = pick_graph(known, inflight_growth);
           if (g2 >= 0) {
             launch_graph(g2);
@@ -269,6 +281,7 @@ class DeviceEngine final : public IEngine {
       reset_counters();
       set_best(best);
       push_host(nodes, n);
+      fresh_ = true;
       return;
     }
     h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
@@ -280,6 +293,7 @@ class DeviceEngine final : public IEngine {
     h_ctl_->overflow = 0;
     ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
     upload_ctl();
+    fresh_ = true;
   }
 
   EngineStats solve_from(const void* nodes, size_t n, int best) override {
@@ -310,8 +324,7 @@ class DeviceEngine final : public IEngine {
       Traits::finalize(a.pool, stream_);
       TTS_HIP_CHECK(hipGetLastError());
       TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
-      inflight_.push_back(m);
-      inflight_k_.push_back(0);
+      push_inflight(m, 0);
       ++stats_.launches;
       sync_ctl();
     }
@@ -400,12 +413,35 @@ class DeviceEngine final : public IEngine {
   void sync_ctl() {
     while (!inflight_.empty()) wait_oldest();
   }
+  // The finalize kernel publishes the mirror's sequence word last (release, system
+  // scope): spinning on it returns as soon as the block is in host memory, without
+  // the completion-signal round trip of hipEventSynchronize. The event is still
+  // queried now and then so a failed graph raises instead of spinning forever.
   void wait_oldest() {
     const auto t0 = std::chrono::steady_clock::now();
     const int m = inflight_.front();
+    const dev::u64 want = inflight_seq_.front();
     inflight_.pop_front();
     inflight_k_.pop_front();
-    TTS_HIP_CHECK(hipEventSynchronize(graph_done_[m]));
+    inflight_seq_.pop_front();
+    if (poll_) {
+      const dev::u64* seq = &h_mirror_[m]->seq;
+      unsigned spins = 0;
+      while (__atomic_load_n(seq, __ATOMIC_ACQUIRE) < want) {
+        __builtin_ia32_pause();
+        if ((++spins & 1023) == 0) {
+          const hipError_t q = hipEventQuery(graph_done_[m]);
+          if (q == hipSuccess) {
+            if (__atomic_load_n(seq, __ATOMIC_ACQUIRE) < want)
+              throw std::runtime_error("graph completed without publishing its control block");
+          } else if (q != hipErrorNotReady) {
+            TTS_HIP_CHECK(q);
+          }
+        }
+      }
+    } else {
+      TTS_HIP_CHECK(hipEventSynchronize(graph_done_[m]));
+    }
     std::memcpy(h_ctl_, h_mirror_[m], sizeof(dev::PoolCtl));
     ++stats_.syncs;
     stats_.t_memcpy += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -414,7 +450,9 @@ class DeviceEngine final : public IEngine {
   // fits, no longer than the pool size suggests: 6 iterations while ramping up or
   // draining, more when the pool holds several parent windows.
   int pick_graph(size_t total, size_t extra) const {
-    size_t want = 6;
+    // right after begin(): one long replay (iters_first) — a graph boundary costs
+    // ~50 us of host sync + relaunch, an empty iteration ~4.5 us (profiles/r1f)
+    size_t want = fresh_ ? std::max<size_t>(6, static_cast<size_t>(cfg_.iters_first)) : 6;
     while (want < static_cast<size_t>(cfg_.iters_large) && total >= (want / 6) * 2 * cfg_.max_parents) want *= 2;
     for (int i = static_cast<int>(ks_.size()) - 1; i >= 0; --i) {
       if (static_cast<size_t>(ks_[i]) > want && i > 0) continue;
@@ -510,9 +548,14 @@ class DeviceEngine final : public IEngine {
       TTS_HIP_CHECK(hipGetLastError());
     }
     TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
+    push_inflight(m, gi);
+    ++stats_.launches;
+    fresh_ = false;
+  }
+  void push_inflight(int m, int gi) {
     inflight_.push_back(m);
     inflight_k_.push_back(gi);
-    ++stats_.launches;
+    inflight_seq_.push_back(++launched_seq_);
   }
 
   hipGraphExec_t capture(int K, int mirror) {
@@ -534,7 +577,7 @@ class DeviceEngine final : public IEngine {
 
   EngineConfig cfg_;
   Args args_;
-  size_t cap_ = 0, buf_nodes_ = 0, max_chunks_ = 0;
+  size_t cap_ = 0, buf_nodes_ = 0, max_chunks_ = 0, spec_min_ = 1;
   int grid_ = 1, cus_ = 0;
   Node* d_ring_ = nullptr;
   Node* d_buf_[2] = {nullptr, nullptr};
@@ -549,6 +592,10 @@ class DeviceEngine final : public IEngine {
   hipEvent_t up_done_ = nullptr;
   int next_mirror_ = 0;
   std::deque<int> inflight_, inflight_k_;
+  std::deque<dev::u64> inflight_seq_;
+  dev::u64 launched_seq_ = 0;  // finalize kernels enqueued (== device ctl->seq when idle)
+  bool poll_ = true;           // spin on the mirror's sequence word (TTS_POLL=0: event sync)
+  bool fresh_ = false;         // no graph launched since begin()
   hipStream_t stream_ = nullptr, own_stream_ = nullptr;
   std::vector<int> ks_;
   std::vector<hipGraphExec_t> graphs_[2];

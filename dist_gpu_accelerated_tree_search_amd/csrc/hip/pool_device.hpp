@@ -39,6 +39,7 @@ struct PoolCtl {
   u64 bot;          // ring base
   u64 pend_children;  // children in the latest buffer (finalize kernel)
   u64 pend_leaves;    // leaves counted by the latest iteration (finalize kernel)
+  u64 seq;            // finalize kernels run so far; published LAST to the host mirror
   int overflow;
   int pad0;
   CtlI32 best;      // incumbent (atomicMin by leaves)
@@ -204,10 +205,14 @@ __global__ __launch_bounds__(kBlock) void pool_gather_strided_kernel(const Node*
 }
 
 // Last node of every graph: counts of the latest buffer for the host.
+// The control block is published to host-mapped memory with system-scope stores,
+// the sequence number last (release): the host polls that word instead of
+// waiting for the graph's completion signal (engine.hpp wait_oldest).
 template <class Node, int MAXCHUNKS>
 __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa) {
   __shared__ PoolSmem<MAXCHUNKS> ps;
   const int n = pa.ctl->nch[0].v;
+  const u64 seq = pa.ctl->seq + 1;
   int c = 0, l = 0;
   for (int i = threadIdx.x; i < n; i += kBlock) {
     c += pa.cnt[0][i];
@@ -219,20 +224,29 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   if (threadIdx.x == 0) {
     pa.ctl->pend_children = static_cast<u64>(ct);
     pa.ctl->pend_leaves = static_cast<u64>(lt);
+    pa.ctl->seq = seq;
   }
-  __syncthreads();
   // publish the whole control block to host-mapped memory: the host reads it
-  // after the graph completes, without a device-to-host copy
+  // without a device-to-host copy
   static_assert(sizeof(PoolCtl) % 4 == 0, "ctl must be dword-sized");
+  constexpr int kPc = static_cast<int>(offsetof(PoolCtl, pend_children) / 4);
+  constexpr int kPl = static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4);
+  constexpr int kSeq = static_cast<int>(offsetof(PoolCtl, seq) / 4);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pa.ctl);
   uint32_t* dst = reinterpret_cast<uint32_t*>(pa.mirror);
   for (int i = threadIdx.x; i < static_cast<int>(sizeof(PoolCtl) / 4); i += kBlock) {
+    if (i == kSeq || i == kSeq + 1) continue;
     uint32_t x = src[i];
-    if (i == static_cast<int>(offsetof(PoolCtl, pend_children) / 4)) x = static_cast<uint32_t>(ct);
-    if (i == static_cast<int>(offsetof(PoolCtl, pend_children) / 4) + 1) x = 0;
-    if (i == static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4)) x = static_cast<uint32_t>(lt);
-    if (i == static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4) + 1) x = 0;
+    if (i == kPc) x = static_cast<uint32_t>(ct);
+    if (i == kPc + 1) x = 0;
+    if (i == kPl) x = static_cast<uint32_t>(lt);
+    if (i == kPl + 1) x = 0;
     __hip_atomic_store(dst + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(&pa.mirror->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -50,7 +50,8 @@ class QueensModel:
         H = ops.require_gpu(device)
         return H.make_queens_engine(self.N, self.G, device=device, max_parents=opts.max_parents,
                                     ring_bytes=opts.ring_bytes, iters_small=opts.iters_small,
-                                    iters_large=opts.iters_large, use_graphs=opts.use_graphs)
+                                    iters_large=opts.iters_large, use_graphs=opts.use_graphs,
+                                    iters_first=opts.iters_first)
 
     def labels_cpu(self, nodes: np.ndarray) -> np.ndarray:
         """labels[i, r] = 1 iff row r is free and diagonal-safe for parent i."""

@@ -33,6 +33,7 @@ class EngineOptions:
     ring_bytes: int = 16 << 30      # device pool capacity
     iters_small: int = 6
     iters_large: int = 48
+    iters_first: int = 24           # first graph replay after begin() (one replay covers a small tree)
     use_graphs: bool = True
     cpu_batch: int = 4096           # CPU engine batch
     cpu_threads: int = 1
@@ -108,7 +109,8 @@ class PfspModel:
         return H.make_pfsp_engine(self.jobs, self.machines, list(self.native.p), self.lb, device=device,
                                   max_parents=opts.max_parents, ring_bytes=opts.ring_bytes,
                                   iters_small=opts.iters_small, iters_large=opts.iters_large,
-                                  use_graphs=opts.use_graphs, taillard_id=self.inst_id)
+                                  use_graphs=opts.use_graphs, taillard_id=self.inst_id,
+                                  iters_first=opts.iters_first)
 
     # ---- bounds (reference evaluate_gpu semantics; used by tests/tools) ----
     def child_bounds_cpu(self, nodes: np.ndarray, best: int = INT_MAX) -> np.ndarray:

@@ -27,6 +27,17 @@ def _env_int(name: str, default: int) -> int:
     return int(v) if v not in (None, "") else default
 
 
+SHM_MAX_VALS = 15  # values per rank in one shared-memory all-gather (ShmControl::kMaxVals)
+
+
+def shm_control_wanted(topo: "Topology") -> bool:
+    """Use the shared-memory control plane when every rank lives on this node
+    (TTS_SHM_CONTROL=0 forces the process-group collectives)."""
+    if os.environ.get("TTS_SHM_CONTROL", "1") == "0":
+        return False
+    return topo.world > 1 and topo.local_world == topo.world and os.path.isdir("/dev/shm")
+
+
 @dataclass
 class Topology:
     rank: int
@@ -69,6 +80,39 @@ class Comm:
         self._buf = None
         self.bytes_sent = 0
         self.bytes_recv = 0
+        self.timeout_s = timeout_s
+        self.ctl = None
+        if shm_control_wanted(self.topo):
+            self.ctl = self._open_shm_control()
+
+    def _open_shm_control(self):
+        """Shared-memory control plane for a single-node job (csrc/core/shm_control.hpp):
+        rank 0 creates a uniquely named segment, the name's nonce travels over the
+        process group once, every rank maps it, then the name is unlinked (nothing
+        is left in /dev/shm, even if a rank dies later)."""
+        from .. import ops
+
+        C = ops.cpu()
+        torch = self.torch
+        nonce = int.from_bytes(os.urandom(6), "little") if self.rank == 0 else 0
+        t = torch.tensor([nonce], dtype=torch.int64, device=self.device)
+        self.dist.broadcast(t, src=0)
+        nonce = int(t.item())
+        name = f"/tts_ctl_{os.getuid()}_{os.environ.get('MASTER_PORT', '0')}_{nonce:x}"
+        ctl = C.ShmControl(name, self.rank, self.world, True) if self.rank == 0 else None
+        self._pg_barrier()
+        if self.rank != 0:
+            ctl = C.ShmControl(name, self.rank, self.world, False)
+        self._pg_barrier()
+        if self.rank == 0:
+            ctl.unlink()
+        return ctl
+
+    def _pg_barrier(self) -> None:
+        if self.use_gpu and self.backend == "nccl":
+            self.dist.barrier(device_ids=[self.topo.local_rank])
+        else:
+            self.dist.barrier()
 
     # ---- basic properties ----
     @property
@@ -89,13 +133,14 @@ class Comm:
 
     def barrier(self) -> None:
         if self.distributed:
-            if self.use_gpu and self.backend == "nccl":
-                self.dist.barrier(device_ids=[self.topo.local_rank])
+            if self.ctl is not None:
+                self.ctl.barrier(self.timeout_s)
             else:
-                self.dist.barrier()
+                self._pg_barrier()
         self.sync_device()
 
     def close(self) -> None:
+        self.ctl = None
         if self._owns_pg and self.dist.is_initialized():
             self.dist.destroy_process_group()
             self._owns_pg = False
@@ -105,6 +150,8 @@ class Comm:
         vals = np.asarray(values, dtype=np.int64).reshape(-1)
         if not self.distributed:
             return vals.reshape(1, -1)
+        if self.ctl is not None and vals.size <= SHM_MAX_VALS:
+            return self.ctl.allgather(vals, self.timeout_s)
         t = self.torch.as_tensor(vals, dtype=self.torch.int64).to(self.device)
         out = self.torch.empty(self.world * vals.size, dtype=self.torch.int64, device=self.device)
         self.dist.all_gather_into_tensor(out, t)
@@ -114,6 +161,9 @@ class Comm:
         vals = np.asarray(values, dtype=np.int64).reshape(-1)
         if not self.distributed:
             return vals
+        if self.ctl is not None and vals.size <= SHM_MAX_VALS:
+            g = self.ctl.allgather(vals, self.timeout_s)
+            return {"sum": g.sum(axis=0), "min": g.min(axis=0), "max": g.max(axis=0)}[op].astype(np.int64)
         t = self.torch.as_tensor(vals, dtype=self.torch.int64).to(self.device)
         rop = {"sum": self.dist.ReduceOp.SUM, "min": self.dist.ReduceOp.MIN, "max": self.dist.ReduceOp.MAX}[op]
         self.dist.all_reduce(t, op=rop)
@@ -123,6 +173,8 @@ class Comm:
         vals = np.asarray(values, dtype=np.float64).reshape(-1)
         if not self.distributed:
             return vals.reshape(1, -1)
+        if self.ctl is not None and vals.size <= SHM_MAX_VALS:
+            return self.ctl.allgather(vals.view(np.int64), self.timeout_s).view(np.float64)
         t = self.torch.as_tensor(vals, dtype=self.torch.float64).to(self.device)
         out = self.torch.empty(self.world * vals.size, dtype=self.torch.float64, device=self.device)
         self.dist.all_gather_into_tensor(out, t)
