@@ -360,6 +360,7 @@ class DeviceEngine final : public IEngine {
       upload_ctl();
     }
     stats_.t_run += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    fresh_ = true;  // the rank's own search starts now: one long first replay
     return dev_total() + spill_.size();
   }
 

@@ -12,6 +12,11 @@ transfer issued by all ranks in the same order:
                       device pool (engine.export_to) into the peer's pool over xGMI;
                       never an all-gather of everybody's nodes.
   * final reduction   all_reduce SUM of counters / MIN of the incumbent.
+When every rank is on this node (torchrun --nnodes=1) the status records, barriers
+and final reductions go through a shared-memory control plane instead
+(csrc/core/shm_control.hpp: ~1 us per all-gather instead of a collective plus two
+host<->device copies); node payloads still go GPU -> GPU over RCCL/xGMI.
+TTS_SHM_CONTROL=0 keeps everything on the process group.
 """
 from __future__ import annotations
 
@@ -94,18 +99,33 @@ class Comm:
 
         C = ops.cpu()
         torch = self.torch
-        nonce = int.from_bytes(os.urandom(6), "little") if self.rank == 0 else 0
-        t = torch.tensor([nonce], dtype=torch.int64, device=self.device)
-        self.dist.broadcast(t, src=0)
-        nonce = int(t.item())
+        ctl, err = None, None
+        nonce = int.from_bytes(os.urandom(6), "little")
         name = f"/tts_ctl_{os.getuid()}_{os.environ.get('MASTER_PORT', '0')}_{nonce:x}"
-        ctl = C.ShmControl(name, self.rank, self.world, True) if self.rank == 0 else None
-        self._pg_barrier()
-        if self.rank != 0:
-            ctl = C.ShmControl(name, self.rank, self.world, False)
-        self._pg_barrier()
         if self.rank == 0:
+            try:
+                ctl = C.ShmControl(name, 0, self.world, True)
+            except Exception as e:  # no /dev/shm, quota, ...: fall back to the process group
+                err = e
+        t = torch.tensor([nonce, int(ctl is not None)], dtype=torch.int64, device=self.device)
+        self.dist.broadcast(t, src=0)
+        nonce, ok0 = (int(x) for x in t.tolist())
+        name = f"/tts_ctl_{os.getuid()}_{os.environ.get('MASTER_PORT', '0')}_{nonce:x}"
+        if self.rank != 0 and ok0:
+            try:
+                ctl = C.ShmControl(name, self.rank, self.world, False)
+            except Exception as e:
+                err = e
+        # every rank must agree on the plane: use it only if all ranks mapped it
+        ok = torch.tensor([int(ctl is not None)], dtype=torch.int64, device=self.device)
+        self.dist.all_reduce(ok, op=self.dist.ReduceOp.MIN)
+        if self.rank == 0 and ctl is not None:
             ctl.unlink()
+        if int(ok.item()) == 0:
+            if err is not None:
+                print(f"[tts] rank {self.rank}: shared-memory control plane unavailable ({err}); "
+                      "using the process group", flush=True)
+            return None
         return ctl
 
     def _pg_barrier(self) -> None:

@@ -44,7 +44,10 @@ class DistConfig:
     # Step 1 on the engines instead of the host: every rank expands the root with
     # the same deterministic warm-up (warm_passes x 6 steps, warm_window parents
     # per step) and keeps the i % world == rank share of the resulting frontier.
-    engine_warmup: bool = True
+    # Off by default: the host BFS to world * init_per_rank nodes costs ~30 us for
+    # 8 ranks on ta014, the device warm-up ~6 dependent iterations plus a sync
+    # and a gather (~80 us), and both give a strided sample of the frontier.
+    engine_warmup: bool = False
     warm_window: int = 2048
     warm_passes: int = 1
     # checkpoint / resume (parallel/checkpoint.py): snapshot every
