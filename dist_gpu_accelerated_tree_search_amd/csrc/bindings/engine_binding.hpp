@@ -100,6 +100,9 @@ inline void bind_engine(py::module_& m) {
             e.begin(a.data(), static_cast<size_t>(a.shape(0)), best);
           },
           py::arg("nodes"), py::arg("best"), "Fresh start from these nodes (counters reset), without running.")
+      .def("set_split", &IEngine::set_split, py::arg("rank"), py::arg("world"), py::arg("min_parents"),
+           "Arm the in-search rank split for the next begin() (see engine_api.hpp).")
+      .def("split_pending", &IEngine::split_pending, py::call_guard<py::gil_scoped_release>())
       .def_property("best", &IEngine::best, &IEngine::set_best)
       .def("reset_counters", &IEngine::reset_counters)
       .def("stats", [](IEngine& e) { return engine_stats_dict(e.stats()); })

@@ -59,6 +59,7 @@ class CpuEngine final : public IEngine {
   long run(long max_launches, double max_seconds, size_t stop_below) override {
     const double t0 = now_s();
     long launches = 0;
+    if (split_world_ > 1 && !split_done_) do_split();
     std::vector<Node> parents(batch_);
     while (!pool_.empty() && pool_.size() >= std::max<size_t>(stop_below, 1)) {
       if (max_launches >= 0 && launches >= max_launches) break;
@@ -78,7 +79,19 @@ class CpuEngine final : public IEngine {
     pool_.clear();
     best_ = best;
     push_host(nodes, n);
+    split_world_ = arm_world_;
+    split_rank_ = arm_rank_;
+    split_min_ = arm_min_;
+    split_done_ = false;
+    arm_world_ = 0;
   }
+  void set_split(int rank, int world, size_t min_parents) override {
+    if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("set_split: bad rank/world");
+    arm_world_ = world;
+    arm_rank_ = rank;
+    arm_min_ = std::max<size_t>(1, min_parents);
+  }
+  bool split_pending() override { return split_world_ > 1 && !split_done_; }
   EngineStats solve_from(const void* nodes, size_t n, int best) override {
     begin(nodes, n, best);
     run(-1, 0.0, 0);
@@ -110,6 +123,7 @@ class CpuEngine final : public IEngine {
     EngineStats s;
     s.tree = tree_;
     s.sol = sol_;
+    if (split_pending() && split_rank_ != 0 && pool_.empty()) s.tree = s.sol = 0;  // see set_split
     s.parents = parents_;
     s.iters = launches_;
     s.launches = launches_;
@@ -120,6 +134,29 @@ class CpuEngine final : public IEngine {
   }
 
  private:
+  // Same contract as the device split: identical breadth-first expansion on every
+  // rank until the pool holds split_min_ nodes, then a strided 1/world share;
+  // ranks != 0 drop the replicated counts. A tree that dies out first is left to
+  // rank 0 (stats()).
+  void do_split() {
+    std::vector<Node> level;
+    while (!pool_.empty() && pool_.size() < split_min_) {
+      level.resize(pool_.size());
+      const size_t n = pool_.pop_back_bulk_free(1, level.size(), level.data(), 1);
+      expand(level.data(), n);
+      parents_ += n;
+    }
+    if (pool_.empty()) return;  // pending forever: rank 0 reports the whole tree
+    std::vector<Node> mine;
+    const size_t n = pool_.size();
+    for (size_t i = static_cast<size_t>(split_rank_); i < n; i += static_cast<size_t>(split_world_))
+      mine.push_back(pool_.data()[i]);
+    pool_.clear();
+    pool_.push_back_bulk_free(mine.data(), mine.size());
+    if (split_rank_ != 0) tree_ = sol_ = 0;
+    split_done_ = true;
+  }
+
   void expand(const Node* parents, size_t n) {
     if (threads_ == 1 || n < 256) {
       for (size_t i = 0; i < n; ++i)
@@ -152,6 +189,9 @@ class CpuEngine final : public IEngine {
   int best_ = 0x7fffffff;
   u64 tree_ = 0, sol_ = 0, parents_ = 0, launches_ = 0;
   double t_run_ = 0;
+  int arm_world_ = 0, arm_rank_ = 0, split_world_ = 0, split_rank_ = 0;
+  size_t arm_min_ = 1, split_min_ = 1;
+  bool split_done_ = false;
 };
 
 // CPU engine that keeps its PFSP instance alive (for callers that build the
@@ -171,6 +211,8 @@ class OwningCpuEngine final : public IEngine {
   void begin(const void* n, size_t k, int b) override { eng_.begin(n, k, b); }
   EngineStats solve_from(const void* n, size_t k, int b) override { return eng_.solve_from(n, k, b); }
   size_t warm_split(int r, int w, size_t win, int p) override { return eng_.warm_split(r, w, win, p); }
+  void set_split(int r, int w, size_t mp) override { eng_.set_split(r, w, mp); }
+  bool split_pending() override { return eng_.split_pending(); }
   void set_best(int b) override { eng_.set_best(b); }
   int best() override { return eng_.best(); }
   void reset_counters() override { eng_.reset_counters(); }

@@ -52,6 +52,15 @@ class IEngine {
   // Counters of the redundant phase are kept by rank 0 only, so the sum over
   // ranks is the explored tree. Returns the pool size kept.
   virtual size_t warm_split(int rank, int world, size_t window, int passes) = 0;
+  // Arm an in-search rank split for the next begin(): every rank begins from the
+  // same nodes; the search runs identically on all ranks until the pool holds at
+  // least `min_parents` nodes, then each rank keeps a disjoint 1/world share of
+  // the next expansion (interleaved per parent) and ranks != 0 drop the counts of
+  // the replicated part. No host round trip and no collective is involved; if the
+  // tree dies out before the split point, rank 0 alone reports it.
+  virtual void set_split(int rank, int world, size_t min_parents) = 0;
+  // An armed split has not happened yet (the pool is still replicated).
+  virtual bool split_pending() = 0;
   virtual void set_best(int b) = 0;
   virtual int best() = 0;
   virtual void reset_counters() = 0;

@@ -93,7 +93,8 @@ class DeviceEngine final : public IEngine {
     int cus = 0;
     TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
     cus_ = cus;
-    const int per_cu = std::max(1, Traits::blocks_per_cu());
+    int per_cu = std::max(1, Traits::blocks_per_cu());
+    if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(g));  // tuning
     grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, static_cast<size_t>(cus) * per_cu)));
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known
@@ -224,7 +225,7 @@ class DeviceEngine final : public IEngine {
     sync_ctl();
     for (;;) {
       // ---- nothing in flight: the host shadow is the device state ----
-      if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
+      check_overflow();
       size_t total = dev_total();
       if (total + spill_.size() == 0) break;
       if (total + spill_.size() < stop_below) break;
@@ -262,7 +263,7 @@ class DeviceEngine final : public IEngine {
           }
         }
         wait_oldest();
-        if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
+        check_overflow();
         known = dev_total();
         inflight_growth = inflight_.empty() ? 0 : static_cast<size_t>(ks_[inflight_k_.front()] + 1) * buf_nodes_;
       }
@@ -277,6 +278,15 @@ class DeviceEngine final : public IEngine {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();
     normalize();
+    // an armed split applies to this solve only
+    h_ctl_->split_world = arm_world_ > 1 ? arm_world_ : 0;
+    h_ctl_->split_rank = arm_rank_;
+    h_ctl_->split_min = arm_min_;
+    for (int i = 0; i < 3; ++i) h_ctl_->slot[i].sdone = 0;
+    const bool armed = arm_world_ > 1;
+    arm_world_ = 0;
+    if (armed && n > cfg_.max_parents)
+      throw std::invalid_argument("set_split: begin() with more nodes than the parent window");
     if (dev_total() != 0 || !spill_.empty() || n > cap_ / 2) {
       reset_counters();
       set_best(best);
@@ -287,8 +297,8 @@ class DeviceEngine final : public IEngine {
     h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
     h_ctl_->best.v = best;
     h_ctl_->bot = 0;
-    h_ctl_->stack[0].v = 0;
-    h_ctl_->nch[0].v = 0;
+    h_ctl_->slot[0].stack = 0;
+    h_ctl_->slot[0].nch = 0;
     h_ctl_->pend_children = h_ctl_->pend_leaves = 0;
     h_ctl_->overflow = 0;
     ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
@@ -350,7 +360,7 @@ class DeviceEngine final : public IEngine {
         }
       }
       h_ctl_->bot = 0;
-      h_ctl_->stack[0].v = keep;
+      h_ctl_->slot[0].stack = keep;
       if (!spill_.empty()) {
         std::vector<Node> mine;
         for (size_t i = rank; i < spill_.size(); i += world) mine.push_back(spill_[i]);
@@ -362,6 +372,21 @@ class DeviceEngine final : public IEngine {
     stats_.t_run += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     fresh_ = true;  // the rank's own search starts now: one long first replay
     return dev_total() + spill_.size();
+  }
+
+  void set_split(int rank, int world, size_t min_parents) override {
+    if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("set_split: bad rank/world");
+    arm_world_ = world;
+    arm_rank_ = rank;
+    // the pool must pass through [min, window] before it can outgrow the window:
+    // one iteration multiplies it by at most the children per parent
+    const size_t per = std::max<size_t>(1, static_cast<size_t>(Traits::kChildrenPerChunk / Traits::kParentsPerChunk));
+    arm_min_ = std::max<size_t>(1, std::min(min_parents, cfg_.max_parents / per));
+  }
+  bool split_pending() override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    sync_ctl();
+    return h_ctl_->split_world > 1 && !h_ctl_->slot[0].sdone;
   }
 
   void set_best(int b) override {
@@ -389,6 +414,9 @@ class DeviceEngine final : public IEngine {
     EngineStats s = stats_;
     s.tree = h_ctl_->tree + h_ctl_->pend_children;
     s.sol = h_ctl_->sol + h_ctl_->pend_leaves;
+    if (h_ctl_->split_world > 1 && !h_ctl_->slot[0].sdone && h_ctl_->split_rank != 0 && dev_total() == 0 &&
+        spill_.empty())
+      s.tree = s.sol = 0;  // the tree died out before the split: every rank explored all of it
     s.parents = h_ctl_->parents;
     s.iters = h_ctl_->iters;
     s.best = h_ctl_->best.v;
@@ -403,7 +431,12 @@ class DeviceEngine final : public IEngine {
   }
 
  private:
-  size_t dev_stack() const { return static_cast<size_t>(h_ctl_->stack[0].v); }
+  void check_overflow() const {
+    if (h_ctl_->overflow == 2)
+      throw std::runtime_error("pool outgrew the parent window before the armed rank split (set_split)");
+    if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
+  }
+  size_t dev_stack() const { return static_cast<size_t>(h_ctl_->slot[0].stack); }
   size_t dev_buf() const { return static_cast<size_t>(h_ctl_->pend_children); }
   size_t dev_total() const { return dev_stack() + dev_buf(); }
 
@@ -475,7 +508,7 @@ class DeviceEngine final : public IEngine {
   void normalize() {
     const size_t c = dev_buf();
     if (c == 0) {
-      h_ctl_->nch[0].v = 0;
+      h_ctl_->slot[0].nch = 0;
       h_ctl_->sol += h_ctl_->pend_leaves;
       h_ctl_->pend_leaves = 0;
       return;
@@ -484,10 +517,10 @@ class DeviceEngine final : public IEngine {
     // the flatten kernel reads the device ctl, which equals the host shadow here
     Traits::flatten(args_.pool, grid_, stream_);
     TTS_HIP_CHECK(hipGetLastError());
-    h_ctl_->stack[0].v += c;
+    h_ctl_->slot[0].stack += c;
     h_ctl_->tree += c;
     h_ctl_->sol += h_ctl_->pend_leaves;
-    h_ctl_->nch[0].v = 0;
+    h_ctl_->slot[0].nch = 0;
     h_ctl_->pend_children = h_ctl_->pend_leaves = 0;
   }
 
@@ -498,7 +531,7 @@ class DeviceEngine final : public IEngine {
     const size_t first = std::min(n, cap_ - start);
     TTS_HIP_CHECK(hipMemcpyAsync(d_ring_ + start, src, first * sizeof(Node), kind, stream_));
     if (first < n) TTS_HIP_CHECK(hipMemcpyAsync(d_ring_, src + first, (n - first) * sizeof(Node), kind, stream_));
-    h_ctl_->stack[0].v += n;
+    h_ctl_->slot[0].stack += n;
   }
 
   void ring_read_bottom(Node* dst, size_t n, hipMemcpyKind kind) {
@@ -509,7 +542,7 @@ class DeviceEngine final : public IEngine {
     if (first < n) TTS_HIP_CHECK(hipMemcpyAsync(dst + first, d_ring_, (n - first) * sizeof(Node), kind, stream_));
     if (kind != hipMemcpyDeviceToDevice) TTS_HIP_CHECK(hipStreamSynchronize(stream_));
     h_ctl_->bot = (h_ctl_->bot + n) & (cap_ - 1);
-    h_ctl_->stack[0].v -= n;
+    h_ctl_->slot[0].stack -= n;
   }
 
   void spill_bottom(size_t n) {
@@ -597,6 +630,8 @@ class DeviceEngine final : public IEngine {
   dev::u64 launched_seq_ = 0;  // finalize kernels enqueued (== device ctl->seq when idle)
   bool poll_ = true;           // spin on the mirror's sequence word (TTS_POLL=0: event sync)
   bool fresh_ = false;         // no graph launched since begin()
+  int arm_world_ = 0, arm_rank_ = 0;  // split armed for the next begin() (set_split)
+  size_t arm_min_ = 1;
   hipStream_t stream_ = nullptr, own_stream_ = nullptr;
   std::vector<int> ks_;
   std::vector<hipGraphExec_t> graphs_[2];

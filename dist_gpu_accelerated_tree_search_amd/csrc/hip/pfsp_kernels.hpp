@@ -314,11 +314,11 @@ template <int NJ, int M, class Smem, class Emit>
 __device__ inline void pfsp_lb1_parent(const PfspArgs<NJ, M>& a, Smem& sm, int p, Emit emit) {
   const PfspNode<NJ>& nd = sm.node[p];
   const int d = nd.depth;
-  int f[M], r[M];
+  int f[M], r[M];  // r: unscheduled work + min tail (see lb1_small_parent)
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     f[m] = (d == 0) ? a.min_heads[m] : 0;
-    r[m] = a.sum_all[m];
+    r[m] = a.sum_all[m] + a.min_tails[m];
   }
   for (int i = 0; i < d; ++i) {
     int pr[M];
@@ -337,12 +337,12 @@ __device__ inline void pfsp_lb1_parent(const PfspArgs<NJ, M>& a, Smem& sm, int p
     load_prow<M>(sm.ptab[job], pr);
     // child front on machine m = s + p[m]; parent remain still holds p[m][job]:
     // max over m of (child front + child remain + min tail)  (ref c_bound_simple.c:219-244)
-    int lb = f[0] + r[0] + a.min_tails[0];
+    int lb = f[0] + r[0];
     int t = f[0] + pr[0];
 #pragma unroll
     for (int m = 1; m < M; ++m) {
       const int s = max(t, f[m]);
-      lb = max(lb, s + r[m] + a.min_tails[m]);
+      lb = max(lb, s + r[m]);
       t = s + pr[m];
     }
     emit(k - d, k, lb);
@@ -397,11 +397,12 @@ __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, 
         int p, k, job;
         const int lb = pfsp_child_bound(a, sm, c, best, p, k, job);
         const bool leaf = sm.node[p].depth + 1 == a.jobs;
+        const bool keep = split_keep(v, first + p, k);
         if (leaf) {
-          ++my_leaves;
+          my_leaves += keep;
           if (lb < best) atomicMin(&pa.ctl->best.v, lb);
         } else {
-          survive = lb < best;
+          survive = keep && lb < best;
         }
       }
       const u64 bal = __ballot(survive);
@@ -472,11 +473,13 @@ template <int NJ, int M, class Emit>
 __device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const uint16_t (*ptab)[PfspConsts<M>::MS],
                                         const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], Emit emit) {
   const int d = static_cast<int>(w[0] & 0xffu);
+  // r[m] = unscheduled work on machine m + its min tail: the tail is folded in
+  // once per parent instead of once per child and machine
   int f[M], r[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     f[m] = (d == 0) ? a.min_heads[m] : 0;
-    r[m] = a.sum_all[m];
+    r[m] = a.sum_all[m] + a.min_tails[m];
   }
 #pragma unroll
   for (int i = 0; i < NJ - 1; ++i) {
@@ -499,12 +502,12 @@ __device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const uint16_t
       const int job = static_cast<int>((w[(1 + k) >> 2] >> (((1 + k) & 3) * 8)) & 0xffu);
       int pr[M];
       load_prow<M>(ptab[job], pr);
-      int lb = f[0] + r[0] + a.min_tails[0];
+      int lb = f[0] + r[0];
       int tt = f[0] + pr[0];
 #pragma unroll
       for (int m = 1; m < M; ++m) {
         const int sv = max(tt, f[m]);
-        lb = max(lb, sv + r[m] + a.min_tails[m]);
+        lb = max(lb, sv + r[m]);
         tt = sv + pr[m];
       }
       emit(k, lb);
@@ -521,17 +524,18 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
   __shared__ PfspSmemLB1s<NJ, M> sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
-  {  // p table -> LDS (made visible by pool_begin's barriers)
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
+  if (v.B == 0 || v.overflow) return;
+  {  // p table -> LDS (visible after the barrier below)
     uint16_t* pt = &sm.ptab[0][0];
     for (int i = tid; i < a.jobs * PfspConsts<M>::MS; i += kBlock) pt[i] = a.ptab[i];
   }
-  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
-  if (v.B == 0 || v.overflow) return;
   const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
   pool_spill_leftovers<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, sm.pool);
+  __syncthreads();
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 gi = static_cast<u64>(ch) * G::BP + tid;
     const bool valid = gi < v.B;
@@ -549,12 +553,21 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
     const bool leaf = d + 1 == a.jobs;
     uint32_t surv = 0;
     int nsurv = 0, nleaf = 0;
+    // child positions this rank keeps (all but in the split iteration); computed
+    // out of the unrolled loop so the hash costs no registers there
+    uint32_t kmask = ~0u;
+    if (v.split) {
+      kmask = 0;
+#pragma unroll 1
+      for (int k = 0; k < NJ; ++k) kmask |= split_keep(v, gi, k) ? (1u << k) : 0u;
+    }
     if (valid) {
       lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+        const bool keep = (kmask >> k) & 1u;
         if (leaf) {
-          ++nleaf;
+          nleaf += keep;
           if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-        } else if (lb < best) {
+        } else if (keep && lb < best) {
           ++nsurv;
           surv |= 1u << k;
         }
@@ -629,11 +642,12 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
     int nsurv = 0, nleaf = 0;
     if (tid < nvalid) {
       const bool leaf = sm.node[tid].depth + 1 == a.jobs;
-      pfsp_lb1_parent<NJ, M>(a, sm, tid, [&](int j, int /*k*/, int lb) {
+      pfsp_lb1_parent<NJ, M>(a, sm, tid, [&](int j, int k, int lb) {
+        const bool keep = split_keep(v, first + tid, k);
         if (leaf) {
-          ++nleaf;
+          nleaf += keep;
           if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-        } else if (lb < best) {
+        } else if (keep && lb < best) {
           ++nsurv;
 #pragma unroll
           for (int q = 0; q < SW; ++q)

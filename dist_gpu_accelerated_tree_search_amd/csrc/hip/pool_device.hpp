@@ -29,8 +29,15 @@ namespace tts {
 namespace dev {
 
 struct PoolCtl {
-  CtlU64 stack[3];  // ring occupancy at the start of iteration t (slot t%3)
-  CtlI32 nch[3];    // chunks written by iteration t-1 into buffer t%2
+  // Rotating per-iteration state, one 128-B line per slot so an iteration's
+  // inputs arrive in one load: iteration t reads slot t%3, workgroup 0 writes
+  // slot (t+1)%3.
+  struct alignas(128) Slot {
+    u64 stack;  // ring occupancy at the start of iteration t
+    int nch;    // chunks written by iteration t-1 into buffer t%2
+    int sdone;  // armed rank split already done (see split_world)
+  };
+  Slot slot[3];
   // plain counters, updated by workgroup 0 (or the host between launches)
   u64 tree;         // pushed children (explored tree), lags one iteration
   u64 sol;          // evaluated leaves (explored solutions), lags one iteration
@@ -40,8 +47,16 @@ struct PoolCtl {
   u64 pend_children;  // children in the latest buffer (finalize kernel)
   u64 pend_leaves;    // leaves counted by the latest iteration (finalize kernel)
   u64 seq;            // finalize kernels run so far; published LAST to the host mirror
-  int overflow;
+  int overflow;       // 1: ring too small, 2: pool outgrew the window before a pending split
+  // In-graph rank split (multi-rank solves): every rank starts from the same nodes
+  // and runs identical iterations until the first one whose window holds at least
+  // split_min parents (and the whole pool); that iteration keeps only the children
+  // whose (parent, position) hash falls on split_rank (split_keep), and ranks != 0
+  // drop the replicated counts gathered so far. Same line as `bot`.
+  int split_world;    // <= 1: no split armed
+  int split_rank;
   int pad0;
+  u64 split_min;
   CtlI32 best;      // incumbent (atomicMin by leaves)
 };
 
@@ -101,7 +116,22 @@ struct IterView {
   u64 S, C, B, nb, ns, L, Snew, bot;
   int nch_in, nchunks;
   bool overflow;
+  bool split;         // this iteration splits the (replicated) pool between ranks
+  int srank, sworld;
 };
+
+// Does this rank keep child position k of window parent gi? (always, outside the
+// split iteration). The owner is a hash of (gi, k) (splitmix64 finalizer): a plain
+// (gi * 1024 + k) % world would hand every child position k to one rank when
+// world divides 1024, and sibling subtrees are strongly correlated in size.
+__device__ inline bool split_keep(const IterView& v, u64 gi, int k) {
+  if (!v.split) return true;
+  u64 x = gi * 1024ull + static_cast<u64>(k) + 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return (x % static_cast<u64>(v.sworld)) == static_cast<u64>(v.srank);
+}
 
 // Everything an iteration needs to know, identical in every workgroup; workgroup
 // 0 also publishes the next slot and folds the previous iteration's counts.
@@ -111,8 +141,22 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   const int b_in = t & 1;
   PoolCtl* ctl = pa.ctl;
   IterView v;
-  v.S = ctl->stack[s_in].v;
-  v.nch_in = ctl->nch[s_in].v;
+  v.S = ctl->slot[s_in].stack;
+  v.nch_in = ctl->slot[s_in].nch;
+  if (v.S == 0 && v.nch_in == 0) {
+    // empty pool (the tail of a replay that outlived its tree): hand the slot on
+    // and leave — no table staging, no scans, no counter traffic
+    v.C = v.B = v.nb = v.ns = v.L = v.Snew = v.bot = 0;
+    v.nchunks = 0;
+    v.overflow = v.split = false;
+    v.srank = v.sworld = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      ctl->slot[s_out].stack = 0;
+      ctl->slot[s_out].nch = 0;
+      ctl->slot[s_out].sdone = ctl->slot[s_in].sdone;
+    }
+    return v;
+  }
   v.bot = ctl->bot;
   v.C = static_cast<u64>(build_prefix(pa.cnt[b_in], v.nch_in, ps));
   v.B = min(v.S + v.C, static_cast<u64>(pa.max_parents));
@@ -122,6 +166,15 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   v.Snew = v.S - v.ns + v.L;
   v.overflow = v.Snew > pa.cap_mask + 1;
   v.nchunks = static_cast<int>((v.B + BP - 1) / BP);
+  const int done_in = ctl->slot[s_in].sdone;
+  v.sworld = ctl->split_world;
+  v.srank = ctl->split_rank;
+  const bool armed = v.sworld > 1 && !done_in && v.B > 0;
+  // a pending split needs the whole (replicated) pool inside the window
+  const bool bad_split = armed && v.B < v.S + v.C;
+  v.split = armed && !bad_split && v.B >= ctl->split_min;
+  const bool overflow = v.overflow;
+  v.overflow = overflow || bad_split;
   if (blockIdx.x == 0) {
     // leaves evaluated by the previous iteration
     int lf = 0;
@@ -129,15 +182,23 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     int lf_total = 0;
     (void)block_exclusive_scan(lf, ps.red, &lf_total);
     if (threadIdx.x == 0) {
-      ctl->stack[s_out].v = v.overflow ? v.S : v.Snew;
-      ctl->nch[s_out].v = v.overflow ? 0 : v.nchunks;
-      ctl->tree += v.C;
-      ctl->sol += static_cast<u64>(lf_total);
+      ctl->slot[s_out].stack = v.overflow ? v.S : v.Snew;
+      ctl->slot[s_out].nch = v.overflow ? 0 : v.nchunks;
+      ctl->slot[s_out].sdone = (done_in || v.split) ? 1 : 0;
+      if (v.split && v.srank != 0) {
+        // everything counted so far was explored identically by every rank: rank 0 keeps it
+        ctl->tree = 0;
+        ctl->sol = 0;
+      } else {
+        ctl->tree += v.C;
+        ctl->sol += static_cast<u64>(lf_total);
+      }
       if (v.B > 0) {
         ctl->parents += v.B;
         ctl->iters += 1;
       }
-      if (v.overflow) ctl->overflow = 1;
+      if (overflow) ctl->overflow = 1;
+      else if (bad_split) ctl->overflow = 2;
     }
   }
   return v;
@@ -179,9 +240,9 @@ template <class Node, int MAXCH, int MAXCHUNKS>
 __global__ __launch_bounds__(kBlock) void pool_flatten_kernel(PoolArgs<Node> pa) {
   __shared__ PoolSmem<MAXCHUNKS> ps;
   IterView v;
-  v.S = pa.ctl->stack[0].v;
+  v.S = pa.ctl->slot[0].stack;
   v.bot = pa.ctl->bot;
-  v.nch_in = pa.ctl->nch[0].v;
+  v.nch_in = pa.ctl->slot[0].nch;
   v.C = static_cast<u64>(build_prefix(pa.cnt[0], v.nch_in, ps));
   v.nb = 0;
   v.L = v.C;
@@ -211,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void pool_gather_strided_kernel(const Node*
 template <class Node, int MAXCHUNKS>
 __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa) {
   __shared__ PoolSmem<MAXCHUNKS> ps;
-  const int n = pa.ctl->nch[0].v;
+  const int n = pa.ctl->slot[0].nch;
   const u64 seq = pa.ctl->seq + 1;
   int c = 0, l = 0;
   for (int i = threadIdx.x; i < n; i += kBlock) {

@@ -90,9 +90,15 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
       const QueensNode nd = *pool_parent<QueensNode, S::MAXCH, S::MAXCHUNKS>(pa, v, t, gi, sm.pool);
       sm.node[tid] = nd;
       if (static_cast<int>(nd.depth) == a.N) {
-        leaf = 1;
+        // a leaf parent of the split iteration is replicated on every rank: rank 0 counts it
+        leaf = (!v.split || v.srank == 0) ? 1 : 0;
       } else {
-        const uint32_t av = queens_free_rows(nd, a.full, a.G);
+        uint32_t av = queens_free_rows(nd, a.full, a.G);
+        if (v.split) {
+          uint32_t keep = 0;
+          for (int r = 0; r < 32; ++r) keep |= split_keep(v, gi, r) ? (1u << r) : 0u;
+          av &= keep;
+        }
         sm.avail[tid] = av;
         nchild = __popc(av);
       }

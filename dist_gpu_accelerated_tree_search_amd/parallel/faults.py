@@ -64,6 +64,10 @@ class Watchdog:
         self.events = 0
         self._timer = None
 
+    @property
+    def enabled(self) -> bool:
+        return self.timeout_s > 0
+
     def arm(self, state: str) -> None:
         if self.timeout_s <= 0:
             return

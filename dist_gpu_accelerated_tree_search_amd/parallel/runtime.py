@@ -50,6 +50,16 @@ class DistConfig:
     engine_warmup: bool = False
     warm_window: int = 2048
     warm_passes: int = 1
+    # Default Step 1 for world > 1: the in-search rank split (engine.set_split).
+    # Every rank begins from the same small host warm-up (the N=1 Step 1) and
+    # searches identically until its pool holds split_per_rank * world nodes;
+    # that expansion is dealt out between ranks on the device, inside the same
+    # graph replay — no host round trip, no collective, no replicated BFS on the
+    # host. False: host BFS to world * init_per_rank nodes + round-robin share.
+    split: bool = True
+    split_per_rank: int = 512    # replicated iterations are narrow and run in parallel on
+                                 # every rank: splitting late costs no latency and deals out
+                                 # ~10^5 subtrees (balance), capped at window / children
     # checkpoint / resume (parallel/checkpoint.py): snapshot every
     # `checkpoint_every` rounds and when `max_rounds` stops the solve early
     checkpoint_dir: str | None = None
@@ -114,6 +124,12 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
         engine.warm_split(rank, world, cfg.warm_window, cfg.warm_passes)
         rs.t_init = time.perf_counter() - t_start
         return _rounds(model, engine, comm, cfg, rs, t_start, best, tree1, sol1)
+    if world > 1 and cfg.split:
+        nodes, tree1, sol1, best = model.warmup(best, cfg.m)
+        engine.set_split(rank, world, cfg.split_per_rank * world)
+        engine.begin(nodes, int(best))
+        rs.t_init = time.perf_counter() - t_start
+        return _rounds(model, engine, comm, cfg, rs, t_start, best, tree1, sol1)
     nodes, tree1, sol1, best = model.warmup(best, world * cfg.init_per_rank)
     mine = np.ascontiguousarray(nodes[round_robin_share(len(nodes), rank, world)])
     rs.t_init = time.perf_counter() - t_start
@@ -149,20 +165,24 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, rs: RankStats, t_start: 
         t1 = time.perf_counter()
         rs.t_run += t1 - t0
         size = engine.size()
+        mybest = engine.best
         faults.before_round()
-        dog.arm(f"rank {rank}/{world} round {rs.rounds + 1} pool {size} best {engine.best}")
-        st = comm.allgather_i64([size, engine.best])
+        if dog.enabled:
+            dog.arm(f"rank {rank}/{world} round {rs.rounds + 1} pool {size} best {mybest}")
+        st = comm.allgather_i64([size, mybest, int(engine.split_pending())])
         dog.disarm()
         rs.rounds += 1
+        # while any pool is still replicated (armed split not reached) nodes must not move
+        replicated = bool(st[:, 2].any())
         gbest = int(st[:, 1].min())
-        if gbest < engine.best:
+        if gbest < mybest:
             engine.best = gbest
         sizes = st[:, 0]
         if int(sizes.sum()) == 0:
             rs.t_comm += time.perf_counter() - t1
             break
         starving = bool((sizes < cfg.m).any())
-        if share and world > 1 and starving:
+        if share and world > 1 and starving and not replicated:
             plan = plan_sharing(sizes, cfg.m, cfg.steal_cap, node_of, intra=cfg.ws, inter=cfg.L)
             plan = faults.filter_plan(plan, rs.rounds)
             if plan:
@@ -178,7 +198,8 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, rs: RankStats, t_start: 
             rs.t_idle += time.perf_counter() - t0
         rs.t_comm += time.perf_counter() - t1
         stop = cfg.max_rounds > 0 and rs.rounds >= cfg.max_rounds
-        if cfg.checkpoint_dir and (stop or (cfg.checkpoint_every > 0 and rs.rounds % cfg.checkpoint_every == 0)):
+        if cfg.checkpoint_dir and not replicated and (stop or (cfg.checkpoint_every > 0 and
+                                                              rs.rounds % cfg.checkpoint_every == 0)):
             est = engine.stats()
             ckpt.save(cfg.checkpoint_dir, rank, world, model, engine,
                       int(est["tree"]) + (tree1 if rank == 0 else 0), int(est["sol"]) + (sol1 if rank == 0 else 0),

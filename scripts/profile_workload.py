@@ -6,7 +6,7 @@ from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel, Queen
 
 which = sys.argv[1] if len(sys.argv) > 1 else "ta014"
 if which == "ta014":
-    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=4 << 30))
+    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=4 << 30))
     for _ in range(20):
         r = solve_engine(m, eng)
 elif which == "ta008":

@@ -149,3 +149,25 @@ def test_watchdog_reports_a_slow_round():
     res = spawn_local(2, solve_rank, (spec,), timeout=300)
     assert (res[0]["tree"], res[0]["sol"]) == (8393, 352)
     assert sum(r["extra"]["watchdog_events"] for r in res) >= 1
+
+
+@pytest.mark.parametrize("world,per_rank", [(2, 1), (3, 16), (4, 200), (3, 10**7)])
+def test_in_search_split_cpu(world, per_rank):
+    # default multi-rank Step 1: identical search on every rank up to the split
+    # point, then a strided share; 10**7 never splits (rank 0 reports the tree)
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu",
+            "dist": {"split": True, "split_per_rank": per_rank}}
+    res = spawn_local(world, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == GOLD
+    per = [w["tree"] for w in res[0]["workers"]]
+    if per_rank < 10**7:
+        assert all(t > 0 for t in per)
+    else:
+        assert per[1:] == [0] * (world - 1)
+
+
+def test_in_search_split_queens_cpu():
+    spec = {"problem": "nqueens", "N": 11, "backend": "cpu", "dist": {"split": True}}
+    res = spawn_local(3, solve_rank, (spec,), timeout=300)
+    assert (res[0]["tree"], res[0]["sol"]) == (166925, 2680)

@@ -112,3 +112,63 @@ def test_warm_split_on_device(world):
         tree += st["tree"]
         sol += st["sol"]
     assert (tree, sol) == GOLDEN[(14, 1)][:2]
+
+
+def _split_solve(model, world, min_parents, opts, nodes, best):
+    """Emulate `world` ranks in one process: one engine per rank on device 0,
+    each armed with the in-search split; returns summed (tree, sol), the per-rank
+    trees and whether every rank left the replicated phase."""
+    tree = sol = 0
+    per, done = [], []
+    for r in range(world):
+        e = model.make_engine("gpu", 0, opts)
+        e.set_split(r, world, min_parents)
+        e.begin(nodes, best)
+        assert e.split_pending()
+        e.run()
+        done.append(not e.split_pending())
+        st = e.stats()
+        tree += st["tree"]
+        sol += st["sol"]
+        per.append(st["tree"])
+        del e
+    return tree, sol, per, done
+
+
+@pytest.mark.parametrize("lb", [1, 0, 2])
+@pytest.mark.parametrize("world,min_parents", [(2, 32), (3, 1536), (8, 4096), (8, 1)])
+def test_in_search_split_golden(lb, world, min_parents):
+    model = PfspModel(14, lb)
+    opts = EngineOptions(ring_bytes=1 << 29, max_parents=1 << 16)
+    nodes, tree1, sol1, best = model.warmup(model.initial_best(1), 25)
+    tree, sol, per, done = _split_solve(model, world, min_parents, opts, nodes, best)
+    assert (tree + tree1, sol + sol1) == GOLDEN[(14, lb)][:2]
+    assert all(done)
+    assert min(per) > 0
+    if lb != 2 and min_parents >= 512 * world:
+        # a late split deals out many subtrees: no rank gets 1.5x the mean
+        assert max(per) < 1.5 * (sum(per) / world), per
+
+
+def test_in_search_split_tree_dies_first():
+    # the pool never reaches the split point (the threshold is clamped to
+    # window / children-per-parent = 16384 here): rank 0 alone reports the tree
+    from dist_gpu_accelerated_tree_search_amd import solve_cpu
+
+    model = QueensModel(7)
+    want = solve_cpu(model)
+    opts = EngineOptions(ring_bytes=1 << 26, max_parents=1 << 19)
+    nodes, tree1, sol1 = model.warmup(0, 4)[:3]
+    tree, sol, per, done = _split_solve(model, 3, 1 << 30, opts, nodes, 0)
+    assert (tree + tree1, sol + sol1) == (want.tree, want.sol)
+    assert per[0] > 0 and per[1] == per[2] == 0 and not any(done)
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_in_search_split_queens(world):
+    model = QueensModel(12)
+    opts = EngineOptions(ring_bytes=1 << 29, max_parents=1 << 16)
+    nodes, tree1, sol1 = model.warmup(0, 25)[:3]
+    tree, sol, per, done = _split_solve(model, world, 16 * world, opts, nodes, 0)
+    assert (tree + tree1, sol + sol1) == (856188, 14200)
+    assert all(done)
