@@ -12,6 +12,7 @@
 #include <memory>
 #include <vector>
 
+#include "../core/pfsp_bounds_cpu.hpp"
 #include "../core/pfsp_instance.hpp"
 #include "engine.hpp"
 #include "pfsp_kernels.hpp"
@@ -49,10 +50,11 @@ struct PfspTraits {
 struct PfspTableImages {
   std::vector<uint16_t> ptab;  // [N][MS]
   std::vector<uint2> recs;     // [P][N]
+  std::vector<uint2> pinfo;    // [P]
 };
 
 template <int NJ, int M>
-inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, M>& a) {
+inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, M>& a, bool pair_order = false) {
   using C = dev::PfspConsts<M>;
   if (in.machines != M) throw std::invalid_argument("machine count does not match kernel instantiation");
   if (in.jobs > NJ) throw std::invalid_argument("job count exceeds kernel bucket");
@@ -71,6 +73,23 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
       rc.x = static_cast<uint32_t>(job) | (static_cast<uint32_t>(in.pt(m0, job)) << 16);
       rc.y = static_cast<uint32_t>(in.pt(m1, job)) | (static_cast<uint32_t>(lag) << 16);
       img.recs[static_cast<size_t>(q) * in.jobs + r] = rc;
+    }
+  }
+  // expand kernel's pair table in the learned early-exit order (lb2_pair_order);
+  // recs stay in the reference order (the bounds kernel keeps its exact partial
+  // values) and pinfo points each slot at its pair's records
+  img.pinfo.resize(C::P);
+  {
+    std::vector<int> ord(C::P);
+    for (int q = 0; q < C::P; ++q) ord[q] = q;
+    if (pair_order) ord = lb2_pair_order(in);
+    for (int i = 0; i < C::P; ++i) {
+      const int q = ord[i];
+      const int m0 = in.pair_m0[q], m1 = in.pair_m1[q];
+      if (in.min_tails[m0] > 0xffff || in.min_tails[m1] > 0xffff)
+        throw std::invalid_argument("LB2 tail does not fit 16 bits");
+      img.pinfo[i].x = static_cast<uint32_t>(m0) | (static_cast<uint32_t>(m1) << 8) | (static_cast<uint32_t>(q) << 16);
+      img.pinfo[i].y = static_cast<uint32_t>(in.min_tails[m0]) | (static_cast<uint32_t>(in.min_tails[m1]) << 16);
     }
   }
   a.jobs = in.jobs;
@@ -102,12 +121,14 @@ template <int NJ, int M, int LBK>
 std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const EngineConfig& cfg) {
   TTS_HIP_CHECK(hipSetDevice(cfg.device));
   dev::PfspArgs<NJ, M> a{};
-  const PfspTableImages img = pfsp_fill_args(in, a);
+  const PfspTableImages img = pfsp_fill_args(in, a, LBK == 2);
   a.ptab = upload_vec(img.ptab);
   a.recs = upload_vec(img.recs);
+  a.pinfo = upload_vec(img.pinfo);
   auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a);
   eng->adopt(const_cast<uint16_t*>(a.ptab));
   eng->adopt(const_cast<uint2*>(a.recs));
+  eng->adopt(const_cast<uint2*>(a.pinfo));
   return eng;
 }
 

@@ -39,8 +39,12 @@ namespace dev {
 template <int NJ, int LBK = 1, int M = 20>
 struct PfspGeom {
   static constexpr int BP1 = NJ <= 50 ? 256 : (NJ <= 100 ? 128 : (NJ <= 200 ? 64 : 32));
-  static constexpr int BP2 = M <= 5 ? BP1 : (M <= 10 ? BP1 / 4 : BP1 / 8);
-  static constexpr int BP = LBK == 2 ? (BP2 > 8 ? BP2 : 8) : BP1;
+  // LB2: parallelism comes from (child, machine pair) tasks, so a chunk only needs
+  // enough children to feed a workgroup; small chunks spread an iteration over
+  // many workgroups and keep the per-chunk LDS (child fronts) small.
+  static constexpr int NM = NJ * M;
+  static constexpr int BP2 = NM <= 100 ? 64 :(NM <= 200 ? 16 : (NM <= 400 ? 8 : (NM <= 1000 ? 4 : 2)));
+  static constexpr int BP = LBK == 2 ? BP2 : BP1;
   static constexpr int MAXCHUNKS = LBK == 2 ? 4096 : 2048;
   static constexpr int MAXCH = BP * NJ;                  // children per chunk (upper bound)
   static constexpr int NWORDS = (MAXCH + 63) / 64;       // survivor bitmap words
@@ -65,6 +69,7 @@ struct PfspArgs {
   PoolArgs<PfspNode<NJ>> pool;  // device-resident pool (pool_device.hpp)
   const uint16_t* ptab;    // job-major p, [jobs][MS]
   const uint2* recs;       // LB2 Johnson records, [P][jobs]: {job | p0<<16, p1 | lag<<16}
+  const uint2* pinfo;      // LB2 pairs in evaluation order: {m0 | m1<<8 | recs pair<<16, tail0 | tail1<<16}
   const int* offsets;      // bounds kernel only: exclusive prefix of child counts
   int* bounds_out;         // bounds kernel only
   const PfspNode<NJ>* parents_in;  // bounds kernel only
@@ -101,8 +106,8 @@ struct PfspSmem {
 // ---------------------------------------------------------------------------
 // Phase A: stage `nvalid` parents (fetched through `src(i)`) and their prefixes.
 // Returns the number of children of the chunk.
-template <int NJ, int M, int LBK, class Src>
-__device__ inline int pfsp_phase_a(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M, LBK>& sm, int nvalid, Src src) {
+template <int NJ, int M, int LBK, class Smem, class Src>
+__device__ inline int pfsp_phase_a(const PfspArgs<NJ, M>& a, Smem& sm, int nvalid, Src src) {
   using G = PfspGeom<NJ, LBK, M>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
@@ -357,20 +362,68 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 
+template <int NJ, int M>
+__device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
+
 template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
-  if constexpr (LBK != 2) {
-    if constexpr (sizeof(PfspNode<NJ>) == 32)
-      pfsp_expand_lb1_small<NJ, M>(a, t);
-    else
-      pfsp_expand_lb1<NJ, M>(a, t);
-    return;
-  }
-  using G = PfspGeom<NJ, LBK, M>;
+  if constexpr (LBK == 2)
+    pfsp_expand_lb2<NJ, M>(a, t);
+  else if constexpr (sizeof(PfspNode<NJ>) == 32)
+    pfsp_expand_lb1_small<NJ, M>(a, t);
+  else
+    pfsp_expand_lb1<NJ, M>(a, t);
+}
+
+// ---------------------------------------------------------------------------
+// LB2 expand. The reference evaluates one child per thread and walks the P machine
+// pairs one after the other (ref bounds_gpu.cu:252-316): O(P*N) dependent steps per
+// lane and, with few children per iteration, a handful of waves on a 256-CU chip.
+// Here the work unit is one (child, machine pair) Johnson walk:
+//   B1  thread-per-child: child front, LB1 of the child from the parent prefix
+//       (O(M)), leaves, and the LB1 filter — LB2 >= LB1 pointwise,
+//       so a child with LB1 >= best is pruned by LB2 as well: only the others enter
+//       the active list (fronts machine-major in LDS, scheduled-set bitmask).
+//   B2  pair-major task loop over (pair q, active child): consecutive lanes share
+//       q, so each Johnson record read is an LDS broadcast; per-pair results are
+//       folded with an LDS atomicMax. A task whose child already exceeds `best`
+//       is skipped (the reference's early exit, c_bound_johnson.c:231-234: only
+//       the lb < best decision matters, and it is unchanged).
+//   B3  survivors (LB2 < best) -> ballot bitmap -> compaction as in every kernel.
+template <int NJ, int M>
+struct PfspSmemLB2 {
+  using G = PfspGeom<NJ, 2, M>;
+  using C = PfspConsts<M>;
+  static constexpr bool kRecsInLds = C::P * NJ * 8 <= 32 * 1024;
+  PfspNode<NJ> node[G::BP];
+  uint32_t fr[G::BP][M];                  // parent front | remain << 16
+  u64 pmask[G::BP][G::NW];                // parent scheduled set
+  int off[G::BP];
+  typename G::map_t map[G::MAXCH];
+  uint16_t ptab[NJ][C::MS];
+  uint16_t cf[M][G::MAXCH];               // active child fronts, machine-major
+  u64 cm[G::MAXCH][G::NW];                // active child scheduled sets
+  int lbv[G::MAXCH];                      // active child LB2 (max over pairs)
+  int16_t act[G::MAXCH];                  // child -> active slot, -1 if decided in B1
+  u64 bits[G::NWORDS + kBlock / kWave];
+  int wpre[kBlock];
+  int scan[kBlock / kWave];
+  int red[kBlock / kWave];
+  uint2 pinfo[C::P];
+  uint2 recs[kRecsInLds ? C::P * NJ : 1];
+  PoolSmem<G::MAXCHUNKS> pool;
+};
+
+template <int NJ, int M>
+__device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
+  using G = PfspGeom<NJ, 2, M>;
+  using C = PfspConsts<M>;
+  using S = PfspSmemLB2<NJ, M>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
   constexpr int NWD = sizeof(Node) / 4;
-  __shared__ PfspSmem<NJ, M, LBK> sm;
+  constexpr int P = C::P;
+  __shared__ S sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
@@ -379,37 +432,115 @@ __global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, 
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-
   pool_spill_leftovers<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, sm.pool);
-  pfsp_stage_tables(a, sm);
+  {  // tables -> LDS (visible after phase A's first barrier)
+    uint16_t* pt = &sm.ptab[0][0];
+    for (int i = tid; i < a.jobs * C::MS; i += kBlock) pt[i] = a.ptab[i];
+    for (int i = tid; i < P; i += kBlock) sm.pinfo[i] = a.pinfo[i];
+    if constexpr (S::kRecsInLds)
+      for (int i = tid; i < P * a.jobs; i += kBlock) sm.recs[i] = a.recs[i];
+  }
+  const uint2* recs = S::kRecsInLds ? sm.recs : a.recs;
+  const int N = a.jobs;
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 first = static_cast<u64>(ch) * G::BP;
     const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), v.B - first));
-    const int total = pfsp_phase_a(a, sm, nvalid, [&](int i) -> const Node* {
+    const int total = pfsp_phase_a<NJ, M, 2>(a, sm, nvalid, [&](int i) -> const Node* {
       return pool_parent<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, first + i, sm.pool);
     });
-    // Phase B: bounds, leaves, survivor bitmap.
-    int my_leaves = 0;
+    // ---- B1: child fronts, LB1 filter, leaves, active list ----
+    int my_leaves = 0, nact = 0;
+    for (int cb = 0; cb < total; cb += kBlock) {
+      const int c = cb + tid;
+      int active = 0, job = 0, p = 0;
+      int f[M];
+      if (c < total) {
+        p = sm.map[c];
+        const int d = sm.node[p].depth;
+        const int k = d + (c - sm.off[p]);
+        job = sm.node[p].prmu[k];
+        int pr[M];
+        load_prow<M>(sm.ptab[job], pr);
+        const uint32_t* fr = sm.fr[p];
+        // LB1 of the child (ref c_bound_simple.c:219-244) and its front
+        int lb1 = static_cast<int>(fr[0] & 0xffff) + static_cast<int>(fr[0] >> 16) + a.min_tails[0];
+        int tt = static_cast<int>(fr[0] & 0xffff) + pr[0];
+        f[0] = tt;
+#pragma unroll
+        for (int m = 1; m < M; ++m) {
+          const int sv = max(tt, static_cast<int>(fr[m] & 0xffff));
+          lb1 = max(lb1, sv + static_cast<int>(fr[m] >> 16) + a.min_tails[m]);
+          tt = sv + pr[m];
+          f[m] = tt;
+        }
+        const bool keep = split_keep(v, first + p, k);
+        if (d + 1 == N) {
+          // a leaf's LB2 is its makespan bound max_m(front + tail) == LB1
+          my_leaves += keep;
+          if (lb1 < best) atomicMin(&pa.ctl->best.v, lb1);
+        } else {
+          active = (keep && lb1 < best) ? 1 : 0;
+        }
+      }
+      int cnt = 0;
+      const int slot = nact + block_exclusive_scan(active, sm.scan, &cnt);
+      if (c < total) sm.act[c] = static_cast<int16_t>(active ? slot : -1);
+      if (active) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) sm.cf[m][slot] = static_cast<uint16_t>(f[m]);
+#pragma unroll
+        for (int w = 0; w < G::NW; ++w)
+          sm.cm[slot][w] = sm.pmask[p][w] | (((job >> 6) == w) ? (1ull << (job & 63)) : 0ull);
+        sm.lbv[slot] = 0;
+      }
+      nact += cnt;
+    }
+    __syncthreads();
+    // ---- B2: (pair, child) Johnson walks, pair-major ----
+    if (nact > 0) {
+      int q = tid / nact, ai = tid - (tid / nact) * nact;
+      const int dq = kBlock / nact, da = kBlock - dq * nact;
+      while (q < P) {
+        if (sm.lbv[ai] <= best) {
+          const uint2 pi = sm.pinfo[q];
+          int t0 = sm.cf[pi.x & 0xff][ai], t1 = sm.cf[(pi.x >> 8) & 0xff][ai];
+          u64 msk[G::NW];
+#pragma unroll
+          for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
+          const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
+#pragma unroll 4
+          for (int r = 0; r < N; ++r) {
+            const uint2 rc = rq[r];
+            const int n0 = t0 + static_cast<int>(rc.x >> 16);
+            const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
+            const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
+            t0 = sched ? t0 : n0;
+            t1 = sched ? t1 : n1;
+          }
+          atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
+        }
+        ai += da;
+        q += dq;
+        if (ai >= nact) {
+          ai -= nact;
+          ++q;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- B3: survivor bitmap ----
     for (int cb = 0; cb < total; cb += kBlock) {
       const int c = cb + tid;
       bool survive = false;
       if (c < total) {
-        int p, k, job;
-        const int lb = pfsp_child_bound(a, sm, c, best, p, k, job);
-        const bool leaf = sm.node[p].depth + 1 == a.jobs;
-        const bool keep = split_keep(v, first + p, k);
-        if (leaf) {
-          my_leaves += keep;
-          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-        } else {
-          survive = keep && lb < best;
-        }
+        const int s = sm.act[c];
+        survive = s >= 0 && sm.lbv[s] < best;
       }
       const u64 bal = __ballot(survive);
       if ((tid & (kWave - 1)) == 0) sm.bits[c >> 6] = bal;
     }
     __syncthreads();
-    // Phase C: compaction into this chunk's slot region + published counts.
+    // ---- C: compaction into this chunk's slot region + published counts ----
     const int nwords = (total + 63) >> 6;
     int nsurv = 0, nleaves = 0;
     const int wp = block_exclusive_scan(tid < nwords ? __popcll(sm.bits[tid]) : 0, sm.scan, &nsurv);
@@ -746,7 +877,8 @@ __global__ __launch_bounds__(kBlock) void pfsp_bounds_kernel(PfspArgs<NJ, M> a) 
     for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
       const int first = ch * G::BP;
       const int nvalid = min(G::BP, a.nparents - first);
-      const int total = pfsp_phase_a(a, sm, nvalid, [&](int i) -> const Node* { return a.parents_in + first + i; });
+      const int total =
+          pfsp_phase_a<NJ, M, LBK>(a, sm, nvalid, [&](int i) -> const Node* { return a.parents_in + first + i; });
       for (int c = tid; c < total; c += kBlock) {
         int p, k, job;
         const int lb = pfsp_child_bound(a, sm, c, a.best_in, p, k, job);
