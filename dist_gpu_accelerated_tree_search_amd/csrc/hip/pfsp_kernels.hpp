@@ -365,8 +365,12 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 
+// Occupancy: the LB1 kernels are latency-bound (profiles/r1o), so the register
+// budget is capped for more resident waves (6 per SIMD for M <= 10: 80 VGPRs, no
+// spills); LB2 is bounded by its LDS footprint instead.
 template <int NJ, int M, int LBK>
-__global__ __launch_bounds__(kBlock) void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK == 2 ? 1 : (M <= 10 ? 6 : 4))))
+void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
     pfsp_expand_lb2<NJ, M>(a, t);
   else if constexpr (sizeof(PfspNode<NJ>) == 32)

@@ -15,6 +15,14 @@ elif which == "ta008":
 elif which == "lb2":
     m = PfspModel(20, 2); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30))
     r = solve_engine(m, eng)
+elif which == "ta056":  # LB2 50x20, time-boxed (the full tree takes far longer)
+    m = PfspModel(56, 2); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30))
+    nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
+    eng.begin(nodes, int(best))
+    eng.run(max_seconds=1.5)
+    st = eng.stats()
+    print(which, st["tree"], st["iters"], "pool", eng.size())
+    raise SystemExit(0)
 elif which == "queens":
     m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30))
     r = solve_engine(m, eng)
