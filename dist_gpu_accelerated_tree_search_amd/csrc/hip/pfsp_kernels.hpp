@@ -659,11 +659,21 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
   __shared__ PfspSmemLB1s<NJ, M> sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
+  // p table loads issued together with pool_begin's (one memory round trip)
+  constexpr int PTN = (NJ * PfspConsts<M>::MS + kBlock - 1) / kBlock;
+  uint16_t ptv[PTN];
+#pragma unroll
+  for (int i = 0; i < PTN; ++i) {
+    const int x = tid + i * kBlock;
+    ptv[i] = x < a.jobs * PfspConsts<M>::MS ? a.ptab[x] : 0;
+  }
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
   if (v.B == 0 || v.overflow) return;
   {  // p table -> LDS (visible after the barrier below)
     uint16_t* pt = &sm.ptab[0][0];
-    for (int i = tid; i < a.jobs * PfspConsts<M>::MS; i += kBlock) pt[i] = a.ptab[i];
+#pragma unroll
+    for (int i = 0; i < PTN; ++i)
+      if (tid + i * kBlock < a.jobs * PfspConsts<M>::MS) pt[tid + i * kBlock] = ptv[i];
   }
   const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   Node* const bout = pa.buf[(t & 1) ^ 1];

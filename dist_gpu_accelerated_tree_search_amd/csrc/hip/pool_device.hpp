@@ -140,9 +140,18 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   const int s_in = t % 3, s_out = (t + 1) % 3;
   const int b_in = t & 1;
   PoolCtl* ctl = pa.ctl;
+  // The slot and the control line are loaded together (one round trip). The
+  // per-chunk counts are read once nch is known: reading the whole window's
+  // counts speculatively in the same round trip made ta014 slower (0.32 -> 0.39
+  // ms, profiles/r1q: cold count lines), though ta008 gained 4 %.
   IterView v;
   v.S = ctl->slot[s_in].stack;
   v.nch_in = ctl->slot[s_in].nch;
+  const int done_in = ctl->slot[s_in].sdone;
+  v.bot = ctl->bot;
+  v.sworld = ctl->split_world;
+  v.srank = ctl->split_rank;
+  const u64 split_min = ctl->split_min;
   if (v.S == 0 && v.nch_in == 0) {
     // empty pool (the tail of a replay that outlived its tree): hand the slot on
     // and leave — no table staging, no scans, no counter traffic
@@ -153,11 +162,10 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       ctl->slot[s_out].stack = 0;
       ctl->slot[s_out].nch = 0;
-      ctl->slot[s_out].sdone = ctl->slot[s_in].sdone;
+      ctl->slot[s_out].sdone = done_in;
     }
     return v;
   }
-  v.bot = ctl->bot;
   v.C = static_cast<u64>(build_prefix(pa.cnt[b_in], v.nch_in, ps));
   v.B = min(v.S + v.C, static_cast<u64>(pa.max_parents));
   v.nb = min(v.B, v.C);
@@ -166,13 +174,10 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   v.Snew = v.S - v.ns + v.L;
   v.overflow = v.Snew > pa.cap_mask + 1;
   v.nchunks = static_cast<int>((v.B + BP - 1) / BP);
-  const int done_in = ctl->slot[s_in].sdone;
-  v.sworld = ctl->split_world;
-  v.srank = ctl->split_rank;
   const bool armed = v.sworld > 1 && !done_in && v.B > 0;
   // a pending split needs the whole (replicated) pool inside the window
   const bool bad_split = armed && v.B < v.S + v.C;
-  v.split = armed && !bad_split && v.B >= ctl->split_min;
+  v.split = armed && !bad_split && v.B >= split_min;
   const bool overflow = v.overflow;
   v.overflow = overflow || bad_split;
   if (blockIdx.x == 0) {

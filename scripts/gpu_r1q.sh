@@ -1,6 +1,6 @@
 #!/bin/bash
-o=gpurun_out/r1p; mkdir -p $o
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_search.py -m gpu -x -q --timeout 120 --timeout-method thread > $o/gpu_tests.log 2>&1 &&
+o=gpurun_out/r1q; mkdir -p $o
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $o/gpu_tests.log 2>&1 &&
 timeout -k 10 200 python -u scripts/lb1_probe.py > $o/lb1_probe.txt 2>&1 &&
 timeout -k 10 120 python bench.py --steps 200 --warmup 20 > $o/n1.json 2> $o/n1.err
 rc=$?
