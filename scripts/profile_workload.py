@@ -9,6 +9,16 @@ if which == "ta014":
     m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=4 << 30))
     for _ in range(20):
         r = solve_engine(m, eng)
+elif which == "ta014_w8":  # rank 0 of an 8-rank split solve (the per-GPU critical path at N=8)
+    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=4 << 30))
+    nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
+    for _ in range(20):
+        eng.set_split(0, 8, 4096)
+        eng.begin(nodes, int(best))
+        eng.run()
+    st = eng.stats()
+    print(which, st["tree"], st["iters"])
+    raise SystemExit(0)
 elif which == "ta008":
     m = PfspModel(8, 0); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30))
     r = solve_engine(m, eng)
