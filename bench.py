@@ -41,7 +41,7 @@ def main() -> int:
     ap.add_argument("--lb", type=int, default=1)
     ap.add_argument("--ub", type=int, default=1)
     ap.add_argument("--max-parents", type=int, default=1 << 19)
-    ap.add_argument("--ring-gb", type=float, default=8.0)
+    ap.add_argument("--ring-gb", type=float, default=32.0)
     ap.add_argument("--init-per-rank", type=int, default=25)
     ap.add_argument("--no-ws", action="store_true", help="static partition (ref -w 0 / -L 0)")
     ap.add_argument("--backend", choices=["gpu", "cpu"], default="gpu")

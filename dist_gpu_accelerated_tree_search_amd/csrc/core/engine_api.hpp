@@ -15,6 +15,8 @@ struct EngineConfig {
   int iters_small = 6;                   // iterations per small graph (multiple of 6)
   int iters_large = 48;                  // iterations per large graph (multiple of 6)
   int iters_first = 24;                  // first replay after begin(): covers a small tree in one graph
+  int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
+  int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };

@@ -90,6 +90,14 @@ class DeviceEngine final : public IEngine {
     pa.cap_mask = cap_ - 1;
     pa.max_parents = static_cast<int>(cfg_.max_parents);
     pa.max_chunks = static_cast<int>(max_chunks_);
+    // two-level iterations (kernels that implement them) for windows up to this many
+    // parents; TTS_FUSE_MAX overrides (0 = off) for A/B runs
+    pa.fuse_max = cfg_.fuse_max;
+    if (const char* f = std::getenv("TTS_FUSE_MAX")) pa.fuse_max = std::max(0, std::atoi(f));
+    pa.local_steps = std::min(cfg_.local_steps, Traits::kLocalSteps);
+    if (const char* f = std::getenv("TTS_LOCAL_STEPS")) pa.local_steps = std::min(std::max(0, std::atoi(f)), Traits::kLocalSteps);
+    pa.local_min = 0;
+    if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
     int cus = 0;
     TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
     cus_ = cus;
@@ -299,7 +307,7 @@ class DeviceEngine final : public IEngine {
     h_ctl_->bot = 0;
     h_ctl_->slot[0].stack = 0;
     h_ctl_->slot[0].nch = 0;
-    h_ctl_->pend_children = h_ctl_->pend_leaves = 0;
+    h_ctl_->pend_children = h_ctl_->pend_leaves = h_ctl_->pend_internal = 0;
     h_ctl_->overflow = 0;
     ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
     upload_ctl();
@@ -380,7 +388,7 @@ class DeviceEngine final : public IEngine {
     arm_rank_ = rank;
     // the pool must pass through [min, window] before it can outgrow the window:
     // one iteration multiplies it by at most the children per parent
-    const size_t per = std::max<size_t>(1, static_cast<size_t>(Traits::kChildrenPerChunk / Traits::kParentsPerChunk));
+    const size_t per = std::max<size_t>(1, static_cast<size_t>(Traits::kMaxChildren));
     arm_min_ = std::max<size_t>(1, std::min(min_parents, cfg_.max_parents / per));
   }
   bool split_pending() override {
@@ -412,7 +420,7 @@ class DeviceEngine final : public IEngine {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();
     EngineStats s = stats_;
-    s.tree = h_ctl_->tree + h_ctl_->pend_children;
+    s.tree = h_ctl_->tree + h_ctl_->pend_children + h_ctl_->pend_internal;
     s.sol = h_ctl_->sol + h_ctl_->pend_leaves;
     if (h_ctl_->split_world > 1 && !h_ctl_->slot[0].sdone && h_ctl_->split_rank != 0 && dev_total() == 0 &&
         spill_.empty())
@@ -510,7 +518,8 @@ class DeviceEngine final : public IEngine {
     if (c == 0) {
       h_ctl_->slot[0].nch = 0;
       h_ctl_->sol += h_ctl_->pend_leaves;
-      h_ctl_->pend_leaves = 0;
+      h_ctl_->tree += h_ctl_->pend_internal;
+      h_ctl_->pend_leaves = h_ctl_->pend_internal = 0;
       return;
     }
     if (dev_stack() + c > cap_) throw std::runtime_error("device ring capacity exceeded");
@@ -518,10 +527,10 @@ class DeviceEngine final : public IEngine {
     Traits::flatten(args_.pool, grid_, stream_);
     TTS_HIP_CHECK(hipGetLastError());
     h_ctl_->slot[0].stack += c;
-    h_ctl_->tree += c;
+    h_ctl_->tree += c + h_ctl_->pend_internal;
     h_ctl_->sol += h_ctl_->pend_leaves;
     h_ctl_->slot[0].nch = 0;
-    h_ctl_->pend_children = h_ctl_->pend_leaves = 0;
+    h_ctl_->pend_children = h_ctl_->pend_leaves = h_ctl_->pend_internal = 0;
   }
 
   void ring_write_top(const Node* src, size_t n, hipMemcpyKind kind) {

@@ -25,13 +25,15 @@ struct PfspTraits {
   using Args = dev::PfspArgs<NJ, M>;
   using G = dev::PfspGeom<NJ, LBK, M>;
   static constexpr int kParentsPerChunk = G::BP;
-  static constexpr int kChildrenPerChunk = G::MAXCH;
+  static constexpr int kChildrenPerChunk = G::SLOT;  // slot region per chunk
+  static constexpr int kMaxChildren = NJ;            // children per parent (one level)
+  static constexpr int kLocalSteps = G::LT;
   static constexpr int kMaxChunks = G::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
   }
   static void flatten(const dev::PoolArgs<Node>& pa, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::MAXCH, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
+    hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::SLOT, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
                        pa);
   }
   static void finalize(const dev::PoolArgs<Node>& pa, hipStream_t s) {

@@ -47,6 +47,12 @@ struct PfspGeom {
   static constexpr int BP = LBK == 2 ? BP2 : BP1;
   static constexpr int MAXCHUNKS = LBK == 2 ? 4096 : 2048;
   static constexpr int MAXCH = BP * NJ;                  // children per chunk (upper bound)
+  // local DFS steps per chunk and iteration (the LB1 register path only) and the
+  // chunk's slot region in the children buffers = its private stack. Two chunks'
+  // worth of children: a chunk keeps stepping while one more full expansion fits,
+  // and the ring's worst-case growth per iteration (engine pick_graph) only doubles.
+  static constexpr int LT = (LBK != 2 && sizeof(PfspNode<NJ>) == 32) ? 8 : 1;
+  static constexpr int SLOT = MAXCH * (LT > 1 ? 2 : 1);
   static constexpr int NWORDS = (MAXCH + 63) / 64;       // survivor bitmap words
   static constexpr int NW = (NJ + 63) / 64;              // 64-bit words of a job set
   using map_t = std::conditional_t<(BP <= 256), uint8_t, uint16_t>;
@@ -436,7 +442,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  pool_spill_leftovers<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, sm.pool);
+  pool_spill_leftovers<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, sm.pool);
   {  // tables -> LDS (visible after phase A's first barrier)
     uint16_t* pt = &sm.ptab[0][0];
     for (int i = tid; i < a.jobs * C::MS; i += kBlock) pt[i] = a.ptab[i];
@@ -450,7 +456,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     const u64 first = static_cast<u64>(ch) * G::BP;
     const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), v.B - first));
     const int total = pfsp_phase_a<NJ, M, 2>(a, sm, nvalid, [&](int i) -> const Node* {
-      return pool_parent<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, first + i, sm.pool);
+      return pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, first + i, sm.pool);
     });
     // ---- B1: child fronts, LB1 filter, leaves, active list ----
     int my_leaves = 0, nact = 0;
@@ -555,7 +561,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       lcnt_out[ch] = nleaves;
     }
     __syncthreads();
-    Node* const dst_chunk = bout + static_cast<size_t>(ch) * G::MAXCH;
+    Node* const dst_chunk = bout + static_cast<size_t>(ch) * G::SLOT;
     for (int c = tid; c < total; c += kBlock) {
       const u64 word = sm.bits[c >> 6];
       if (!((word >> (c & 63)) & 1ull)) continue;
@@ -597,8 +603,12 @@ __device__ inline uint32_t node_byte(const uint32_t (&w)[sizeof(PfspNode<NJ>) / 
 template <int NJ, int M>
 struct PfspSmemLB1s {
   using G = PfspGeom<NJ, 1>;
+  // two-level iterations: parents per chunk such that their children fit one per
+  // thread and their grandchildren fit the chunk's MAXCH slots
+  static constexpr int BPF = (kBlock / NJ) < (G::MAXCH / (NJ * (NJ - 1))) ? (kBlock / NJ) : (G::MAXCH / (NJ * (NJ - 1)));
   uint16_t ptab[NJ][PfspConsts<M>::MS];
   int scan[kBlock / kWave];
+  uint4 mid[kBlock][2];  // level-1 survivors of a two-level chunk
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -650,6 +660,181 @@ __device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const uint16_t
   }
 }
 
+// Children of the parent held in w whose positions are set in surv, written as
+// consecutive 32-B nodes from dst (node words in registers, element 0 = depth).
+template <int NJ>
+__device__ inline void emit_children(const uint32_t (&w)[8], uint32_t surv, uint4* dst) {
+  const int d = static_cast<int>(w[0] & 0xffu);
+  const uint32_t jd = node_byte<NJ>(w, 1 + d);
+  uint32_t base[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) base[i] = w[i];
+  base[0] = (base[0] & ~0xffu) | static_cast<uint32_t>(d + 1);
+  while (surv) {
+    const int k = __ffs(surv) - 1;
+    surv &= surv - 1;
+    uint32_t c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = base[i];
+    node_set<NJ>(c, 1 + d, node_byte<NJ>(w, 1 + k));
+    node_set<NJ>(c, 1 + k, jd);
+    dst[0] = make_uint4(c[0], c[1], c[2], c[3]);
+    dst[1] = make_uint4(c[4], c[5], c[6], c[7]);
+    dst += 2;
+  }
+}
+
+// Two-level chunk loop (v.fused): BPF parents per chunk, one per thread of the
+// first wave, expanded into LDS (level 1: survivors are pushed-and-popped tree
+// nodes, counted in the chunk's leaf word), then every level-1 survivor — one per
+// thread — is expanded and its survivors go to the chunk's slot region. Same
+// counting rules as the one-level loop: leaves at either level lower the
+// incumbent and count as solutions.
+template <int NJ, int M>
+__device__ inline void lb1_small_two_level(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ, M>& sm, const IterView& v,
+                                           int t, int best) {
+  using G = PfspGeom<NJ, 1>;
+  using Node = PfspNode<NJ>;
+  constexpr int BPF = PfspSmemLB1s<NJ, M>::BPF;
+  const int tid = threadIdx.x;
+  const auto& pa = a.pool;
+  Node* const bout = pa.buf[(t & 1) ^ 1];
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+    uint32_t w[8];
+    const u64 gi = static_cast<u64>(ch) * BPF + tid;
+    const bool valid = tid < BPF && gi < v.B;
+    if (valid) {
+      const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool));
+      const uint4 x0 = src[0], x1 = src[1];
+      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+    }
+    uint32_t surv = 0;
+    int nsurv = 0, nleaf = 0;
+    if (valid) {
+      const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
+      lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+        if (leaf) {
+          ++nleaf;
+          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+        } else if (lb < best) {
+          ++nsurv;
+          surv |= 1u << k;
+        }
+      });
+    }
+    int tot1 = 0;
+    const int off1 = block_exclusive_scan(nsurv, sm.scan, &tot1);
+    if (surv) emit_children<NJ>(w, surv, &sm.mid[off1][0]);
+    __syncthreads();
+    surv = 0;
+    nsurv = 0;
+    if (tid < tot1) {
+      const uint4 x0 = sm.mid[tid][0], x1 = sm.mid[tid][1];
+      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+      const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
+      lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+        if (leaf) {
+          ++nleaf;
+          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+        } else if (lb < best) {
+          ++nsurv;
+          surv |= 1u << k;
+        }
+      });
+    }
+    int tot = 0;
+    const int off = block_exclusive_scan(nsurv | (nleaf << 16), sm.scan, &tot) & 0xffff;
+    if (tid == 0) {
+      cnt_out[ch] = tot & 0xffff;
+      lcnt_out[ch] = (tot >> 16) | (tot1 << 16);
+    }
+    if (surv) emit_children<NJ>(w, surv, reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off));
+  }
+}
+
+// Local DFS chunk loop (v.local): chunk ch takes v.bp window parents, then keeps
+// popping up to kBlock nodes from the top of its own slot region (its private stack,
+// written by this workgroup only and read back through L2) and pushing their
+// survivors there, for up to pa.local_steps steps or until the stack is empty. The
+// stack left is the chunk's output (cnt), the nodes pushed and expanded in between
+// are explored tree nodes (high half of the leaf word). Pops read slots
+// [top - n, top) and pushes write from top - n on: every pop is in registers before
+// the scan's barrier that precedes the first push.
+template <int NJ, int M>
+__device__ inline void lb1_small_local(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ, M>& sm, const IterView& v, int t,
+                                       int best) {
+  using G = PfspGeom<NJ, 1>;
+  using Node = PfspNode<NJ>;
+  const int tid = threadIdx.x;
+  const auto& pa = a.pool;
+  Node* const bout = pa.buf[(t & 1) ^ 1];
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  const int steps = pa.local_steps;
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+    uint4* const stk = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
+    int top = 0, pushed = 0, nleaf = 0;
+    for (int s = 0; s < steps; ++s) {
+      uint32_t w[8];
+      bool valid;
+      if (s == 0) {
+        const u64 gi = static_cast<u64>(ch) * v.bp + tid;
+        valid = tid < v.bp && gi < v.B;
+        if (valid) {
+          const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool));
+          const uint4 x0 = src[0], x1 = src[1];
+          w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+          w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+        }
+      } else {
+        if (top == 0) break;  // uniform
+        const int npop = min(top, kBlock);
+        valid = tid < npop;
+        if (valid) {
+          const uint4* src = stk + 2 * (top - npop + tid);
+          const uint4 x0 = src[0], x1 = src[1];
+          w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+          w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+        }
+        top -= npop;
+      }
+      uint32_t surv = 0;
+      int nsurv = 0;
+      if (valid) {
+        const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
+        lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+          if (leaf) {
+            ++nleaf;
+            if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+          } else if (lb < best) {
+            ++nsurv;
+            surv |= 1u << k;
+          }
+        });
+      }
+      int tot = 0;
+      const int off = block_exclusive_scan(nsurv, sm.scan, &tot);
+      if (surv) emit_children<NJ>(w, surv, stk + 2 * (top + off));
+      top += tot;
+      pushed += tot;
+      // pushes visible to the next step's pops (workgroup scope), and room left
+      // for one more full step
+      __syncthreads();
+      if (top + kBlock * NJ > G::SLOT) break;
+    }
+    int leaves = 0;
+    (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
+    if (tid == 0) {
+      cnt_out[ch] = top;
+      lcnt_out[ch] = leaves | ((pushed - top) << 16);
+    }
+  }
+}
+
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
   using G = PfspGeom<NJ, 1>;
@@ -667,7 +852,7 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
     const int x = tid + i * kBlock;
     ptv[i] = x < a.jobs * PfspConsts<M>::MS ? a.ptab[x] : 0;
   }
-  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, PfspSmemLB1s<NJ, M>::BPF, G::LT);
   if (v.B == 0 || v.overflow) return;
   {  // p table -> LDS (visible after the barrier below)
     uint16_t* pt = &sm.ptab[0][0];
@@ -679,14 +864,22 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  pool_spill_leftovers<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, sm.pool);
+  pool_spill_leftovers<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, sm.pool);
   __syncthreads();
+  if (v.local) {
+    lb1_small_local<NJ, M>(a, sm, v, t, best);
+    return;
+  }
+  if (v.fused) {
+    lb1_small_two_level<NJ, M>(a, sm, v, t, best);
+    return;
+  }
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 gi = static_cast<u64>(ch) * G::BP + tid;
     const bool valid = gi < v.B;
     uint32_t w[NWD];
     if (valid) {
-      const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, gi, sm.pool));
+      const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool));
       const uint4 x0 = src[0], x1 = src[1];
       w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
       w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
@@ -731,7 +924,7 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
 #pragma unroll
       for (int i = 0; i < NWD; ++i) base[i] = w[i];
       base[0] = (base[0] & ~0xffu) | static_cast<uint32_t>(d + 1);
-      uint4* dst = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::MAXCH + off);
+      uint4* dst = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off);
       while (surv) {
         const int k = __ffs(surv) - 1;
         surv &= surv - 1;
@@ -766,7 +959,7 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  pool_spill_leftovers<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, sm.pool);
+  pool_spill_leftovers<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, sm.pool);
   {
     constexpr int MS = PfspConsts<M>::MS;
     uint16_t* pt = &sm.ptab[0][0];
@@ -778,7 +971,7 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
     for (int x = tid; x < nvalid * VPN; x += kBlock) {
       const int i = x / VPN, w = x - i * VPN;
       reinterpret_cast<uint4*>(&sm.node[i])[w] =
-          reinterpret_cast<const uint4*>(pool_parent<Node, G::MAXCH, G::MAXCHUNKS>(pa, v, t, first + i, sm.pool))[w];
+          reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, first + i, sm.pool))[w];
     }
     __syncthreads();
     u64 surv[SW];
@@ -815,7 +1008,7 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
       for (int i = 0; i < NWD; ++i) w[i] = reinterpret_cast<const uint32_t*>(&nd)[i];
       const uint32_t jd = nd.prmu[d];
       node_set<NJ>(w, 0, static_cast<uint32_t>(d + 1));
-      Node* dst = bout + static_cast<size_t>(ch) * G::MAXCH + off;
+      Node* dst = bout + static_cast<size_t>(ch) * G::SLOT + off;
 #pragma unroll
       for (int q = 0; q < SW; ++q) {
         u64 m = surv[q];

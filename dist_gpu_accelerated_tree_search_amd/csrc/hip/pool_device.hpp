@@ -46,6 +46,7 @@ struct PoolCtl {
   u64 bot;          // ring base
   u64 pend_children;  // children in the latest buffer (finalize kernel)
   u64 pend_leaves;    // leaves counted by the latest iteration (finalize kernel)
+  u64 pend_internal;  // children pushed and expanded inside the latest (two-level) iteration
   u64 seq;            // finalize kernels run so far; published LAST to the host mirror
   int overflow;       // 1: ring too small, 2: pool outgrew the window before a pending split
   // In-graph rank split (multi-rank solves): every rank starts from the same nodes
@@ -71,7 +72,15 @@ struct PoolArgs {
   u64 cap_mask;
   int max_parents;
   int max_chunks;
+  int fuse_max;     // two-level iterations for windows of at most this many parents (0: off)
+  int local_steps;  // > 1: local DFS iterations of up to this many steps per chunk (kernels that have them)
+  int local_min;    // local DFS for windows of at least this many parents (0: grid x chunk)
 };
+
+// Per-chunk leaf word: leaves in the low 16 bits; the high 16 bits count the
+// children a two-level iteration pushed and expanded itself (explored tree).
+__device__ inline int lcnt_leaves(int x) { return x & 0xffff; }
+__device__ inline int lcnt_inner(int x) { return static_cast<int>(static_cast<uint32_t>(x) >> 16); }
 
 template <int MAXCHUNKS>
 struct PoolSmem {
@@ -117,6 +126,9 @@ struct IterView {
   int nch_in, nchunks;
   bool overflow;
   bool split;         // this iteration splits the (replicated) pool between ranks
+  bool fused;         // two-level iteration: chunks of BPF parents, grandchildren out
+  bool local;         // local DFS iteration: each chunk runs up to pa.local_steps steps on its own stack
+  int bp;             // window parents per chunk
   int srank, sworld;
 };
 
@@ -136,7 +148,19 @@ __device__ inline bool split_keep(const IterView& v, u64 gi, int k) {
 // Everything an iteration needs to know, identical in every workgroup; workgroup
 // 0 also publishes the next slot and folds the previous iteration's counts.
 template <class Node, int MAXCHUNKS>
-__device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, PoolSmem<MAXCHUNKS>& ps) {
+//
+// Two-level iterations (BPF > 0, kernels that implement them): a window of at most
+// pa.fuse_max parents, outside a pending rank split, is expanded two tree levels
+// deep in chunks of BPF parents — one dependent kernel instead of two where an
+// iteration is latency-bound (few parents), same chunk slot layout.
+//
+// Local DFS iterations (LT > 1 and pa.local_steps > 1): the window is dealt out over
+// the grid (chunks of at most BP parents) and each workgroup keeps expanding the top
+// of its chunk's own slot region — a private stack in L2 — for up to local_steps
+// levels; what is left on the stack is the chunk's output. Several tree levels per
+// dependent kernel, and the next iteration re-deals the stacks over the grid.
+__device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, PoolSmem<MAXCHUNKS>& ps,
+                                      int BPF = 0, int LT = 1) {
   const int s_in = t % 3, s_out = (t + 1) % 3;
   const int b_in = t & 1;
   PoolCtl* ctl = pa.ctl;
@@ -157,7 +181,8 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     // and leave — no table staging, no scans, no counter traffic
     v.C = v.B = v.nb = v.ns = v.L = v.Snew = v.bot = 0;
     v.nchunks = 0;
-    v.overflow = v.split = false;
+    v.overflow = v.split = v.fused = v.local = false;
+    v.bp = BP;
     v.srank = v.sworld = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       ctl->slot[s_out].stack = 0;
@@ -168,24 +193,47 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   }
   v.C = static_cast<u64>(build_prefix(pa.cnt[b_in], v.nch_in, ps));
   v.B = min(v.S + v.C, static_cast<u64>(pa.max_parents));
+  const bool armed = v.sworld > 1 && !done_in && v.B > 0;
+  // Local DFS when the pool holds a backlog of pa.local_min parents (default: four
+  // grid-filling windows of BP-parent chunks), never while the pool is replicated
+  // (the split must see every level). Below that, breadth (one level per kernel,
+  // every chunk short) keeps the grid busier than chunks that step for different
+  // lengths. A local window is one chunk per workgroup, at most BP parents each: a
+  // workgroup's steps are not queued behind another chunk's.
+  const u64 full = static_cast<u64>(gridDim.x) * BP;
+  const u64 lmin = pa.local_min > 0 ? static_cast<u64>(pa.local_min) : 4 * full;
+  v.local = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= max(lmin, full);
+  if (v.local) v.B = min(v.B, full);
   v.nb = min(v.B, v.C);
   v.ns = v.B - v.nb;
   v.L = v.C - v.nb;
   v.Snew = v.S - v.ns + v.L;
   v.overflow = v.Snew > pa.cap_mask + 1;
-  v.nchunks = static_cast<int>((v.B + BP - 1) / BP);
-  const bool armed = v.sworld > 1 && !done_in && v.B > 0;
   // a pending split needs the whole (replicated) pool inside the window
   const bool bad_split = armed && v.B < v.S + v.C;
   v.split = armed && !bad_split && v.B >= split_min;
+  v.fused = !v.local && BPF > 0 && !armed && v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
+  int bp = v.fused ? BPF : BP;
+  if (v.local) {
+    // spread a window smaller than the grid over every workgroup
+    const u64 per = (v.B + gridDim.x - 1) / gridDim.x;
+    bp = static_cast<int>(min(static_cast<u64>(BP), max(per, 1ull)));
+  }
+  v.bp = bp;
+  v.nchunks = static_cast<int>((v.B + bp - 1) / bp);
   const bool overflow = v.overflow;
   v.overflow = overflow || bad_split;
   if (blockIdx.x == 0) {
     // leaves evaluated by the previous iteration
-    int lf = 0;
-    for (int i = threadIdx.x; i < v.nch_in; i += kBlock) lf += pa.lcnt[b_in][i];
-    int lf_total = 0;
+    int lf = 0, in = 0;
+    for (int i = threadIdx.x; i < v.nch_in; i += kBlock) {
+      const int x = pa.lcnt[b_in][i];
+      lf += lcnt_leaves(x);
+      in += lcnt_inner(x);
+    }
+    int lf_total = 0, in_total = 0;
     (void)block_exclusive_scan(lf, ps.red, &lf_total);
+    (void)block_exclusive_scan(in, ps.scan, &in_total);
     if (threadIdx.x == 0) {
       ctl->slot[s_out].stack = v.overflow ? v.S : v.Snew;
       ctl->slot[s_out].nch = v.overflow ? 0 : v.nchunks;
@@ -195,7 +243,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
         ctl->tree = 0;
         ctl->sol = 0;
       } else {
-        ctl->tree += v.C;
+        ctl->tree += v.C + static_cast<u64>(in_total);
         ctl->sol += static_cast<u64>(lf_total);
       }
       if (v.B > 0) {
@@ -279,17 +327,21 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   __shared__ PoolSmem<MAXCHUNKS> ps;
   const int n = pa.ctl->slot[0].nch;
   const u64 seq = pa.ctl->seq + 1;
-  int c = 0, l = 0;
+  int c = 0, l = 0, in = 0;
   for (int i = threadIdx.x; i < n; i += kBlock) {
     c += pa.cnt[0][i];
-    l += pa.lcnt[0][i];
+    const int x = pa.lcnt[0][i];
+    l += lcnt_leaves(x);
+    in += lcnt_inner(x);
   }
-  int ct = 0, lt = 0;
+  int ct = 0, lt = 0, it = 0;
   (void)block_exclusive_scan(c, ps.scan, &ct);
   (void)block_exclusive_scan(l, ps.red, &lt);
+  (void)block_exclusive_scan(in, ps.scan, &it);
   if (threadIdx.x == 0) {
     pa.ctl->pend_children = static_cast<u64>(ct);
     pa.ctl->pend_leaves = static_cast<u64>(lt);
+    pa.ctl->pend_internal = static_cast<u64>(it);
     pa.ctl->seq = seq;
   }
   // publish the whole control block to host-mapped memory: the host reads it
@@ -297,6 +349,7 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   static_assert(sizeof(PoolCtl) % 4 == 0, "ctl must be dword-sized");
   constexpr int kPc = static_cast<int>(offsetof(PoolCtl, pend_children) / 4);
   constexpr int kPl = static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4);
+  constexpr int kPi = static_cast<int>(offsetof(PoolCtl, pend_internal) / 4);
   constexpr int kSeq = static_cast<int>(offsetof(PoolCtl, seq) / 4);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pa.ctl);
   uint32_t* dst = reinterpret_cast<uint32_t*>(pa.mirror);
@@ -307,6 +360,8 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
     if (i == kPc + 1) x = 0;
     if (i == kPl) x = static_cast<uint32_t>(lt);
     if (i == kPl + 1) x = 0;
+    if (i == kPi) x = static_cast<uint32_t>(it);
+    if (i == kPi + 1) x = 0;
     __hip_atomic_store(dst + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();

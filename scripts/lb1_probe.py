@@ -9,7 +9,7 @@ from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel, solve
 GOLD = {(14, 1): (2573652, 2648, 1377), (8, 0): (113458723, 808498, 1206)}
 for key, reps in (((14, 1), 60), ((8, 0), 3)):
     m = PfspModel(*key)
-    eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=8 << 30))
+    eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=32 << 30))
     ts = []
     for _ in range(reps):
         r = solve_engine(m, eng)

@@ -6,11 +6,11 @@ from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel, Queen
 
 which = sys.argv[1] if len(sys.argv) > 1 else "ta014"
 if which == "ta014":
-    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=4 << 30))
+    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=32 << 30))
     for _ in range(20):
         r = solve_engine(m, eng)
 elif which == "ta014_w8":  # rank 0 of an 8-rank split solve (the per-GPU critical path at N=8)
-    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=4 << 30))
+    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=32 << 30))
     nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
     for _ in range(20):
         eng.set_split(0, 8, 4096)
@@ -20,13 +20,13 @@ elif which == "ta014_w8":  # rank 0 of an 8-rank split solve (the per-GPU critic
     print(which, st["tree"], st["iters"])
     raise SystemExit(0)
 elif which == "ta008":
-    m = PfspModel(8, 0); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30))
+    m = PfspModel(8, 0); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=32 << 30))
     r = solve_engine(m, eng)
 elif which == "lb2":
-    m = PfspModel(20, 2); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30))
+    m = PfspModel(20, 2); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=32 << 30))
     r = solve_engine(m, eng)
 elif which == "ta056":  # LB2 50x20, time-boxed (the full tree takes far longer)
-    m = PfspModel(56, 2); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30))
+    m = PfspModel(56, 2); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=32 << 30))
     nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
     eng.begin(nodes, int(best))
     eng.run(max_seconds=1.5)
@@ -34,6 +34,6 @@ elif which == "ta056":  # LB2 50x20, time-boxed (the full tree takes far longer)
     print(which, st["tree"], st["iters"], "pool", eng.size())
     raise SystemExit(0)
 elif which == "queens":
-    m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30))
+    m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=32 << 30))
     r = solve_engine(m, eng)
 print(which, r.tree, r.sol, r.best, f"{r.elapsed*1e3:.2f} ms")

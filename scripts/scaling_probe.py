@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     model = QueensModel(a.queens) if a.queens else PfspModel(a.inst, a.lb)
-    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=4 << 30))
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=32 << 30))
     best = model.initial_best(1)
     nodes, t1, s1, b1 = model.warmup(best, 25)
     for _ in range(5):

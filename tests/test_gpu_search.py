@@ -46,12 +46,19 @@ def test_engine_reuse_graphs_off_and_small_windows():
 
 
 def test_spill_and_refill_with_unknown_optimum():
-    # -u 0 grows a much larger pool; a 1-MB ring forces host spill + refill
+    # -u 0 grows a larger pool on a small ring
     model = PfspModel(14, 0)
     eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=1 << 20, iters_large=12))
     r = solve_engine(model, eng, ub=0)
-    st = eng.stats()
     assert r.best == 1377
+    # a host frontier larger than half the ring (the ring is raised to 8 windows of
+    # children, 2^19 nodes here) is spilled to the host on begin() and refilled
+    # while the device drains: the golden tree survives the round trip
+    model = PfspModel(14, 1)
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=1 << 20, iters_large=12))
+    r = solve_engine(model, eng, ub=1, m=400_000)
+    assert (r.tree, r.sol, r.best) == GOLDEN[(14, 1)]
+    st = eng.stats()
     assert st["spilled"] > 0 and st["refilled"] > 0
 
 
@@ -172,3 +179,24 @@ def test_in_search_split_queens(world):
     tree, sol, per, done = _split_solve(model, world, 16 * world, opts, nodes, 0)
     assert (tree + tree1, sol + sol1) == (856188, 14200)
     assert all(done)
+
+
+@pytest.mark.parametrize("local,fuse", [("0", "0"), ("0", None), ("2", None), (None, None)])
+def test_lb1_iteration_modes(monkeypatch, local, fuse):
+    """One-level, two-level (fused) and local-DFS iterations of the LB1 register
+    kernel (TTS_LOCAL_STEPS / TTS_FUSE_MAX, read when the engine is built) explore
+    the same trees: LB1 and LB1_d, a small window, and the spill path."""
+    for k, v in (("TTS_LOCAL_STEPS", local), ("TTS_FUSE_MAX", fuse)):
+        if v is None:
+            monkeypatch.delenv(k, raising=False)
+        else:
+            monkeypatch.setenv(k, v)
+    for key in ((14, 1), (12, 0), (7, 0)):
+        r = solve_gpu(PfspModel(*key), ub=1, opts=SMALL)
+        assert (r.tree, r.sol, r.best) == GOLDEN[key]
+    r = solve_gpu(PfspModel(8, 0), opts=SMALL)
+    assert (r.tree, r.sol, r.best) == (113458723, 808498, 1206)
+    model = PfspModel(14, 1)
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=1 << 20, iters_large=12))
+    r = solve_engine(model, eng)
+    assert (r.tree, r.sol, r.best) == GOLDEN[(14, 1)]
