@@ -17,6 +17,9 @@ struct EngineConfig {
   int iters_first = 24;                  // first replay after begin(): covers a small tree in one graph
   int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
   int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
+  int narrow_bp = 16;                    // narrow local DFS for windows of <= this many parents per workgroup
+  int narrow_steps = 0;                  // ... up to this many steps per chunk (<= 1: off; measured slower)
+  int narrow_cap = 512;                  // ... while the chunk's stack holds <= this many nodes
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };

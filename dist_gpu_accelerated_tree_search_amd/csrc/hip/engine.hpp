@@ -98,6 +98,12 @@ class DeviceEngine final : public IEngine {
     if (const char* f = std::getenv("TTS_LOCAL_STEPS")) pa.local_steps = std::min(std::max(0, std::atoi(f)), Traits::kLocalSteps);
     pa.local_min = 0;
     if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
+    pa.narrow_bp = cfg_.narrow_bp;
+    pa.narrow_steps = std::min(cfg_.narrow_steps, Traits::kLocalSteps > 1 ? 64 : 0);
+    pa.narrow_cap = cfg_.narrow_cap;
+    if (const char* f = std::getenv("TTS_NARROW_BP")) pa.narrow_bp = std::max(0, std::atoi(f));
+    if (const char* f = std::getenv("TTS_NARROW_STEPS")) pa.narrow_steps = std::max(0, std::atoi(f));
+    if (const char* f = std::getenv("TTS_NARROW_CAP")) pa.narrow_cap = std::max(0, std::atoi(f));
     int cus = 0;
     TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
     cus_ = cus;

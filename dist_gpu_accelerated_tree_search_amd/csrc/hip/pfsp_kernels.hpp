@@ -774,7 +774,7 @@ __device__ inline void lb1_small_local(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  const int steps = pa.local_steps;
+  const int steps = v.steps;
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     uint4* const stk = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
     int top = 0, pushed = 0, nleaf = 0;
@@ -824,7 +824,7 @@ __device__ inline void lb1_small_local(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ
       // pushes visible to the next step's pops (workgroup scope), and room left
       // for one more full step
       __syncthreads();
-      if (top + kBlock * NJ > G::SLOT) break;
+      if (top + kBlock * NJ > G::SLOT || top > v.cap) break;
     }
     int leaves = 0;
     (void)block_exclusive_scan(nleaf, sm.scan, &leaves);

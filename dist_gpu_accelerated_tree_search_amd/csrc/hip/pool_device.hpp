@@ -74,7 +74,10 @@ struct PoolArgs {
   int max_chunks;
   int fuse_max;     // two-level iterations for windows of at most this many parents (0: off)
   int local_steps;  // > 1: local DFS iterations of up to this many steps per chunk (kernels that have them)
-  int local_min;    // local DFS for windows of at least this many parents (0: grid x chunk)
+  int local_min;    // wide local DFS when the pool holds at least this many parents (0: 4 grid windows)
+  int narrow_bp;    // narrow local DFS for windows of at most narrow_bp parents per workgroup (0: off)
+  int narrow_steps; // ... of up to this many steps per chunk
+  int narrow_cap;   // ... while the chunk's stack holds at most this many nodes
 };
 
 // Per-chunk leaf word: leaves in the low 16 bits; the high 16 bits count the
@@ -127,8 +130,10 @@ struct IterView {
   bool overflow;
   bool split;         // this iteration splits the (replicated) pool between ranks
   bool fused;         // two-level iteration: chunks of BPF parents, grandchildren out
-  bool local;         // local DFS iteration: each chunk runs up to pa.local_steps steps on its own stack
+  bool local;         // local DFS iteration: each chunk steps on its own stack
   int bp;             // window parents per chunk
+  int steps;          // local DFS: steps per chunk at most
+  int cap;            // local DFS: no further step once the stack holds more than this
   int srank, sworld;
 };
 
@@ -183,6 +188,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     v.nchunks = 0;
     v.overflow = v.split = v.fused = v.local = false;
     v.bp = BP;
+    v.steps = v.cap = 0;
     v.srank = v.sworld = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       ctl->slot[s_out].stack = 0;
@@ -200,9 +206,20 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // every chunk short) keeps the grid busier than chunks that step for different
   // lengths. A local window is one chunk per workgroup, at most BP parents each: a
   // workgroup's steps are not queued behind another chunk's.
+  //
+  // Narrow local DFS for windows of at most pa.narrow_bp parents per workgroup (the
+  // ramp-up, the tail, a rank's share after a split): every workgroup follows its
+  // few subtrees for up to pa.narrow_steps levels — a level costs one LDS/L2 step
+  // instead of one dependent kernel — and hands its stack back to the grid as soon
+  // as it holds more than pa.narrow_cap nodes (the subtree turned wide).
   const u64 full = static_cast<u64>(gridDim.x) * BP;
   const u64 lmin = pa.local_min > 0 ? static_cast<u64>(pa.local_min) : 4 * full;
-  v.local = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= max(lmin, full);
+  const bool wide = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= max(lmin, full);
+  const bool narrow = !wide && LT > 1 && pa.narrow_steps > 1 && !armed &&
+                      v.B <= static_cast<u64>(gridDim.x) * static_cast<u64>(pa.narrow_bp);
+  v.local = wide || narrow;
+  v.steps = wide ? pa.local_steps : pa.narrow_steps;
+  v.cap = wide ? 0x7fffffff : pa.narrow_cap;
   if (v.local) v.B = min(v.B, full);
   v.nb = min(v.B, v.C);
   v.ns = v.B - v.nb;

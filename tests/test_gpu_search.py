@@ -181,16 +181,20 @@ def test_in_search_split_queens(world):
     assert all(done)
 
 
-@pytest.mark.parametrize("local,fuse", [("0", "0"), ("0", None), ("2", None), (None, None)])
-def test_lb1_iteration_modes(monkeypatch, local, fuse):
+@pytest.mark.parametrize("env", [
+    {"TTS_LOCAL_STEPS": "0", "TTS_FUSE_MAX": "0"},                    # one level per kernel
+    {"TTS_LOCAL_STEPS": "0"},                                         # + two-level small windows
+    {"TTS_LOCAL_STEPS": "2", "TTS_LOCAL_MIN": "1"},                   # wide local DFS everywhere
+    {"TTS_NARROW_STEPS": "16", "TTS_NARROW_CAP": "256"},              # narrow local DFS
+    {}])                                                              # defaults
+def test_lb1_iteration_modes(monkeypatch, env):
     """One-level, two-level (fused) and local-DFS iterations of the LB1 register
-    kernel (TTS_LOCAL_STEPS / TTS_FUSE_MAX, read when the engine is built) explore
-    the same trees: LB1 and LB1_d, a small window, and the spill path."""
-    for k, v in (("TTS_LOCAL_STEPS", local), ("TTS_FUSE_MAX", fuse)):
-        if v is None:
-            monkeypatch.delenv(k, raising=False)
-        else:
-            monkeypatch.setenv(k, v)
+    kernel (TTS_* knobs, read when the engine is built) explore the same trees:
+    LB1 and LB1_d, a small window, and the spill path."""
+    for k in ("TTS_LOCAL_STEPS", "TTS_FUSE_MAX", "TTS_LOCAL_MIN", "TTS_NARROW_STEPS", "TTS_NARROW_CAP"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     for key in ((14, 1), (12, 0), (7, 0)):
         r = solve_gpu(PfspModel(*key), ub=1, opts=SMALL)
         assert (r.tree, r.sol, r.best) == GOLDEN[key]
