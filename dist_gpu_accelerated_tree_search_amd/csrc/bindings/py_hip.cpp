@@ -100,7 +100,7 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("device") = 0,
       py::arg("max_parents") = size_t(1) << 18, py::arg("ring_bytes") = size_t(16) << 30, py::arg("iters_small") = 6,
       py::arg("iters_large") = 48, py::arg("use_graphs") = true, py::arg("stream") = 0, py::arg("taillard_id") = 0,
-      py::arg("iters_first") = 24);
+      py::arg("iters_first") = 18);
 
   m.def(
       "make_queens_engine",

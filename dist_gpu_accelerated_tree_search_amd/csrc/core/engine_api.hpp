@@ -14,7 +14,7 @@ struct EngineConfig {
   size_t ring_bytes = size_t(16) << 30;  // device ring capacity in bytes (rounded down to 2^k nodes)
   int iters_small = 6;                   // iterations per small graph (multiple of 6)
   int iters_large = 48;                  // iterations per large graph (multiple of 6)
-  int iters_first = 24;                  // first replay after begin(): covers a small tree in one graph
+  int iters_first = 18;                  // first replay after begin(): covers a 20-job tree in one graph
   int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
   int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
   int narrow_bp = 16;                    // narrow local DFS for windows of <= this many parents per workgroup

@@ -124,11 +124,17 @@ class DeviceEngine final : public IEngine {
     }
     // graphs of 6, 12, 24, ... iterations up to iters_large; run() picks one from
     // the pool size and the worst-case ring growth
-    for (int k = cfg_.iters_small; k <= cfg_.iters_large; k *= 2) {
-      ks_.push_back(k);
-      if (cfg_.use_graphs)
-        for (int m = 0; m < 2; ++m) graphs_[m].push_back(capture(k, m));
+    // (and the first replay's length, when it is not one of them)
+    if (const char* f = std::getenv("TTS_ITERS_FIRST")) cfg_.iters_first = std::max(6, std::atoi(f) / 6 * 6);
+    for (int k = cfg_.iters_small; k <= cfg_.iters_large; k *= 2) ks_.push_back(k);
+    if (cfg_.iters_first % 6 == 0 && cfg_.iters_first < cfg_.iters_large &&
+        std::find(ks_.begin(), ks_.end(), cfg_.iters_first) == ks_.end()) {
+      ks_.push_back(cfg_.iters_first);
+      std::sort(ks_.begin(), ks_.end());
     }
+    if (cfg_.use_graphs)
+      for (int k : ks_)
+        for (int m = 0; m < 2; ++m) graphs_[m].push_back(capture(k, m));
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
     stats_.t_malloc = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
