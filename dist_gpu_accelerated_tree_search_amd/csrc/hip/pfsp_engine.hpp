@@ -9,6 +9,7 @@
 // and are owned (freed) by the engine.
 #pragma once
 
+#include <cstdlib>
 #include <memory>
 #include <vector>
 
@@ -127,6 +128,10 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   a.ptab = upload_vec(img.ptab);
   a.recs = upload_vec(img.recs);
   a.pinfo = upload_vec(img.pinfo);
+  // wave-uniform pair walks measured 2.6x slower on ta056 (active children per chunk
+  // fill a fraction of a wave, profiles/r1af): dense (pair, child) tasks by default
+  a.lb2_wave = 0;
+  if (const char* f = std::getenv("TTS_LB2_WAVE")) a.lb2_wave = std::atoi(f) != 0;  // A/B runs
   auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a);
   eng->adopt(const_cast<uint16_t*>(a.ptab));
   eng->adopt(const_cast<uint2*>(a.recs));

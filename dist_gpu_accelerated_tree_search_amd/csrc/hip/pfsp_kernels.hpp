@@ -82,6 +82,7 @@ struct PfspArgs {
   int jobs;
   int nparents;            // bounds kernel only
   int best_in;             // bounds kernel only
+  int lb2_wave;            // LB2 expand: wave-uniform pair walks (1) or dense (pair, child) tasks (0)
   int min_heads[M];
   int min_tails[M];
   int sum_all[M];
@@ -424,6 +425,56 @@ struct PfspSmemLB2 {
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
+// B2, wave-uniform variant: a wave walks ONE machine pair for up to 64 active
+// children (lane = child). The pair's Johnson records are then the same for every
+// lane, so they are read with scalar loads (constant address space: the tables are
+// written once, before the engine's first launch) into SGPRs and enter the VALU as
+// scalar operands. The dense variant above spends a per-lane 8-B load (L2 latency:
+// the 50x20 tables are 76 KB, larger than L1) plus its unpacking on every step.
+// Cost: lanes past the active count idle (a chunk's active list is rarely a whole
+// number of waves). profiles/r1ae (dense: 60 % of wave cycles waiting); measured
+// 2.6x slower on ta056 (profiles/r1af: active children per chunk fill a fraction of
+// a wave), so it is off by default (TTS_LB2_WAVE=1 turns it on).
+using kconst_u64 = const __attribute__((address_space(4))) unsigned long long;  // {x, y} of a uint2
+
+template <int NJ, int M, class S>
+__device__ inline void lb2_walks_wave(const PfspArgs<NJ, M>& a, S& sm, int nact, int best) {
+  using G = PfspGeom<NJ, 2, M>;
+  constexpr int P = PfspConsts<M>::P;
+  constexpr int NWAVE = kBlock / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+  kconst_u64* const pinfo = (kconst_u64*)(uintptr_t)a.pinfo;
+  kconst_u64* const recs = (kconst_u64*)(uintptr_t)a.recs;
+  const int N = a.jobs;
+  for (int base = 0; base < nact; base += kWave) {
+    const int ai = base + lane;
+    const int aic = ai < nact ? ai : nact - 1;
+    for (int q = wave; q < P; q += NWAVE) {
+      const bool on = ai < nact && sm.lbv[aic] <= best;
+      if (__ballot(on) == 0) continue;
+      const u64 piw = pinfo[q];
+      const uint2 pi = make_uint2(static_cast<uint32_t>(piw), static_cast<uint32_t>(piw >> 32));
+      int t0 = sm.cf[pi.x & 0xff][aic], t1 = sm.cf[(pi.x >> 8) & 0xff][aic];
+      u64 msk[G::NW];
+#pragma unroll
+      for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[aic][w];
+      kconst_u64* const rq = recs + static_cast<int>(pi.x >> 16) * N;
+#pragma unroll 8
+      for (int r = 0; r < N; ++r) {
+        const u64 rw = rq[r];
+        const uint32_t rx = static_cast<uint32_t>(rw), ry = static_cast<uint32_t>(rw >> 32);
+        const int n0 = t0 + static_cast<int>(rx >> 16);
+        const int n1 = max(t1, n0 + static_cast<int>(ry >> 16)) + static_cast<int>(ry & 0xffff);
+        const bool sched = job_in<G::NW>(msk, static_cast<int>(rx & 0xffff));
+        t0 = sched ? t0 : n0;
+        t1 = sched ? t1 : n1;
+      }
+      if (on) atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
+    }
+  }
+}
+
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   using G = PfspGeom<NJ, 2, M>;
@@ -507,7 +558,9 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     }
     __syncthreads();
     // ---- B2: (pair, child) Johnson walks, pair-major ----
-    if (nact > 0) {
+    if (nact > 0 && a.lb2_wave) {
+      lb2_walks_wave<NJ, M>(a, sm, __builtin_amdgcn_readfirstlane(nact), best);
+    } else if (nact > 0) {
       int q = tid / nact, ai = tid - (tid / nact) * nact;
       const int dq = kBlock / nact, da = kBlock - dq * nact;
       while (q < P) {

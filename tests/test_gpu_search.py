@@ -28,6 +28,22 @@ def test_pfsp_bigger_trees_on_gpu():
     assert (r.tree, r.sol, r.best) == (8122579, 0, 1108)
 
 
+# 50x20 LB2 (the 50-job bucket, 190 machine pairs) with an incumbent below the optimum:
+# the trees stay small. Golden values from this repo's CPU engine (LB2 oracle, the
+# reference's lb2_bound semantics); ta056 -u 1 itself has no known tree size.
+TA056_TIGHT = {140: (78361, 0, 3539), 135: (454770, 0, 3544)}
+
+
+@pytest.mark.parametrize("wave", ["1", "0"])
+def test_ta056_lb2_tight_incumbent(wave, monkeypatch):
+    monkeypatch.setenv("TTS_LB2_WAVE", wave)  # wave-uniform pair walks / dense (pair, child) tasks
+    model = PfspModel(56, 2)
+    eng = model.make_engine("gpu", 0, SMALL)
+    for gap, gold in TA056_TIGHT.items():
+        r = solve_engine(model, eng, best=model.best_known - gap)
+        assert (r.tree, r.sol, r.best) == gold, (wave, gap)
+
+
 @pytest.mark.parametrize("N,gold", [(8, (2056, 92)), (12, (856188, 14200)), (14, (27358552, 365596)),
                                     (15, (171129071, 2279184))])
 def test_queens_golden_on_gpu(N, gold):
