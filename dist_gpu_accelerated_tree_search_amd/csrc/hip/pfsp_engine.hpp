@@ -9,6 +9,7 @@
 // and are owned (freed) by the engine.
 #pragma once
 
+#include <algorithm>
 #include <cstdlib>
 #include <memory>
 #include <vector>
@@ -132,6 +133,15 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   // fill a fraction of a wave, profiles/r1af): dense (pair, child) tasks by default
   a.lb2_wave = 0;
   if (const char* f = std::getenv("TTS_LB2_WAVE")) a.lb2_wave = std::atoi(f) != 0;  // A/B runs
+  {  // packed LDS records for the leading pairs, when every field fits its bits. Off by
+     // default: 0.055 vs 0.057 G nodes/s on ta056 (profiles/r1ag) — the walks do not
+     // wait on the record loads. TTS_LB2_LDS_PAIRS=<n> turns it on for A/B runs.
+    bool fits = in.jobs <= 64;
+    for (const uint2& rc : img.recs) fits = fits && (rc.x >> 16) < 128 && (rc.y & 0xffff) < 128 && (rc.y >> 16) < 4096;
+    const int cap = fits ? std::min(dev::PfspSmemLB2<NJ, M>::kPackPairs, dev::PfspConsts<M>::P) : 0;
+    a.lb2_lds_pairs = 0;
+    if (const char* f = std::getenv("TTS_LB2_LDS_PAIRS")) a.lb2_lds_pairs = std::max(0, std::min(std::atoi(f), cap));
+  }
   auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a);
   eng->adopt(const_cast<uint16_t*>(a.ptab));
   eng->adopt(const_cast<uint2*>(a.recs));

@@ -82,12 +82,15 @@ struct PfspArgs {
   int jobs;
   int nparents;            // bounds kernel only
   int best_in;             // bounds kernel only
-  int lb2_wave;            // LB2 expand: wave-uniform pair walks (1) or dense (pair, child) tasks (0)
   int min_heads[M];
   int min_tails[M];
   int sum_all[M];
   uint8_t pm0[PfspConsts<M>::P];
   uint8_t pm1[PfspConsts<M>::P];
+  // LB2 expand variants (A/B knobs, both off by default; after the tables so the
+  // LB1 kernels' argument layout is unchanged)
+  int lb2_wave;            // wave-uniform pair walks (1) or dense (pair, child) tasks (0)
+  int lb2_lds_pairs;       // leading pairs whose packed records are staged in LDS
 };
 
 template <int NJ, int M, int LBK>
@@ -406,6 +409,12 @@ struct PfspSmemLB2 {
   using G = PfspGeom<NJ, 2, M>;
   using C = PfspConsts<M>;
   static constexpr bool kRecsInLds = C::P * NJ * 8 <= 32 * 1024;
+  // Otherwise (50x20: 76 KB of records) the records of the first kPackPairs pairs in
+  // evaluation order — the ones most walks reach before the early exit — are kept
+  // in LDS packed to 4 B {job:6 | p0:7 | p1:7 | lag:12}, in the LDS left over below
+  // the 4-workgroups-per-CU limit (40 KB). The host enables it (lb2_lds_pairs) only
+  // when every value fits.
+  static constexpr int kPackPairs = (kRecsInLds || NJ > 64) ? 0 : (7 * 1024) / (4 * NJ);
   PfspNode<NJ> node[G::BP];
   uint32_t fr[G::BP][M];                  // parent front | remain << 16
   u64 pmask[G::BP][G::NW];                // parent scheduled set
@@ -422,6 +431,7 @@ struct PfspSmemLB2 {
   int red[kBlock / kWave];
   uint2 pinfo[C::P];
   uint2 recs[kRecsInLds ? C::P * NJ : 1];
+  uint32_t rpk[kPackPairs > 0 ? kPackPairs * NJ : 1];
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -500,9 +510,16 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     for (int i = tid; i < P; i += kBlock) sm.pinfo[i] = a.pinfo[i];
     if constexpr (S::kRecsInLds)
       for (int i = tid; i < P * a.jobs; i += kBlock) sm.recs[i] = a.recs[i];
+    if constexpr (S::kPackPairs > 0)
+      for (int i = tid; i < a.lb2_lds_pairs * a.jobs; i += kBlock) {
+        const int slot = i / a.jobs, r = i - slot * a.jobs;
+        const uint2 rc = a.recs[static_cast<int>(a.pinfo[slot].x >> 16) * a.jobs + r];
+        sm.rpk[i] = (rc.x & 0xffffu) | ((rc.x >> 16) << 6) | ((rc.y & 0xffffu) << 13) | ((rc.y >> 16) << 20);
+      }
   }
   const uint2* recs = S::kRecsInLds ? sm.recs : a.recs;
   const int N = a.jobs;
+  const int npk = S::kPackPairs > 0 ? a.lb2_lds_pairs : 0;
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 first = static_cast<u64>(ch) * G::BP;
     const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), v.B - first));
@@ -570,15 +587,28 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
           u64 msk[G::NW];
 #pragma unroll
           for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
-          const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
+          if (q < npk) {  // packed records in LDS
+            const uint32_t* rq = sm.rpk + q * N;
 #pragma unroll 4
-          for (int r = 0; r < N; ++r) {
-            const uint2 rc = rq[r];
-            const int n0 = t0 + static_cast<int>(rc.x >> 16);
-            const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
-            const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
-            t0 = sched ? t0 : n0;
-            t1 = sched ? t1 : n1;
+            for (int r = 0; r < N; ++r) {
+              const uint32_t w = rq[r];
+              const int n0 = t0 + static_cast<int>((w >> 6) & 127u);
+              const int n1 = max(t1, n0 + static_cast<int>(w >> 20)) + static_cast<int>((w >> 13) & 127u);
+              const bool sched = job_in<G::NW>(msk, static_cast<int>(w & 63u));
+              t0 = sched ? t0 : n0;
+              t1 = sched ? t1 : n1;
+            }
+          } else {
+            const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
+#pragma unroll 4
+            for (int r = 0; r < N; ++r) {
+              const uint2 rc = rq[r];
+              const int n0 = t0 + static_cast<int>(rc.x >> 16);
+              const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
+              const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
+              t0 = sched ? t0 : n0;
+              t1 = sched ? t1 : n1;
+            }
           }
           atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
         }

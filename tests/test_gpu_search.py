@@ -34,9 +34,10 @@ def test_pfsp_bigger_trees_on_gpu():
 TA056_TIGHT = {140: (78361, 0, 3539), 135: (454770, 0, 3544)}
 
 
-@pytest.mark.parametrize("wave", ["1", "0"])
-def test_ta056_lb2_tight_incumbent(wave, monkeypatch):
+@pytest.mark.parametrize("wave,lds", [("0", "0"), ("1", "0"), ("0", "64")])
+def test_ta056_lb2_tight_incumbent(wave, lds, monkeypatch):
     monkeypatch.setenv("TTS_LB2_WAVE", wave)  # wave-uniform pair walks / dense (pair, child) tasks
+    monkeypatch.setenv("TTS_LB2_LDS_PAIRS", lds)  # packed LDS records for the leading pairs
     model = PfspModel(56, 2)
     eng = model.make_engine("gpu", 0, SMALL)
     for gap, gold in TA056_TIGHT.items():
