@@ -43,9 +43,12 @@ struct PfspGeom {
   // enough children to feed a workgroup; small chunks spread an iteration over
   // many workgroups and keep the per-chunk LDS (child fronts) small.
   static constexpr int NM = NJ * M;
-  static constexpr int BP2 = NM <= 100 ? 64 :(NM <= 200 ? 16 : (NM <= 400 ? 8 : (NM <= 1000 ? 4 : 2)));
+  static constexpr int BP2 = NM <= 100 ? 64 :(NM <= 200 ? 16 : (NM <= 1000 ? 8 : 2));
   static constexpr int BP = LBK == 2 ? BP2 : BP1;
-  static constexpr int MAXCHUNKS = LBK == 2 ? 4096 : 2048;
+  // 50-job LB2 (NM 500..1000): 8-parent chunks, half as many per iteration (same
+  // 16K-parent window, half the per-chunk barriers; the smaller chunk-count prefix
+  // pays for the larger child arrays in LDS)
+  static constexpr int MAXCHUNKS = LBK == 2 ? (NM > 400 && NM <= 1000 ? 2048 : 4096) : 2048;
   static constexpr int MAXCH = BP * NJ;                  // children per chunk (upper bound)
   // local DFS steps per chunk and iteration (the LB1 register path only) and the
   // chunk's slot region in the children buffers = its private stack. Two chunks'
@@ -414,7 +417,7 @@ struct PfspSmemLB2 {
   // in LDS packed to 4 B {job:6 | p0:7 | p1:7 | lag:12}, in the LDS left over below
   // the 4-workgroups-per-CU limit (40 KB). The host enables it (lb2_lds_pairs) only
   // when every value fits.
-  static constexpr int kPackPairs = (kRecsInLds || NJ > 64) ? 0 : (7 * 1024) / (4 * NJ);
+  static constexpr int kPackPairs = (kRecsInLds || NJ > 64) ? 0 : (3 * 1024) / (4 * NJ);
   PfspNode<NJ> node[G::BP];
   uint32_t fr[G::BP][M];                  // parent front | remain << 16
   u64 pmask[G::BP][G::NW];                // parent scheduled set
