@@ -133,6 +133,11 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   // fill a fraction of a wave, profiles/r1af): dense (pair, child) tasks by default
   a.lb2_wave = 0;
   if (const char* f = std::getenv("TTS_LB2_WAVE")) a.lb2_wave = std::atoi(f) != 0;  // A/B runs
+  // B2 in rounds of pairs: ta056 (50x20) 0.060 -> 0.081 G nodes/s, ta020 (20x10)
+  // 11.1 -> 8.0 ms, ta014 (20x10) even; ta010 (20x5, 10 pairs) 4.0 -> 4.6 ms
+  // (profiles/r1ak): on from 10 machines (45 pairs)
+  a.lb2_rounds = M >= 10 ? 1 : 0;
+  if (const char* f = std::getenv("TTS_LB2_ROUNDS")) a.lb2_rounds = std::atoi(f) != 0;  // A/B runs
   {  // packed LDS records for the leading pairs, when every field fits its bits. Off by
      // default: 0.055 vs 0.057 G nodes/s on ta056 (profiles/r1ag) — the walks do not
      // wait on the record loads. TTS_LB2_LDS_PAIRS=<n> turns it on for A/B runs.

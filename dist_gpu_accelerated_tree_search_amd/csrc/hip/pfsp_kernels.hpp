@@ -94,6 +94,7 @@ struct PfspArgs {
   // LB1 kernels' argument layout is unchanged)
   int lb2_wave;            // wave-uniform pair walks (1) or dense (pair, child) tasks (0)
   int lb2_lds_pairs;       // leading pairs whose packed records are staged in LDS
+  int lb2_rounds;          // B2 in rounds of pairs, re-compacting the children still below best
 };
 
 template <int NJ, int M, int LBK>
@@ -428,6 +429,7 @@ struct PfspSmemLB2 {
   u64 cm[G::MAXCH][G::NW];                // active child scheduled sets
   int lbv[G::MAXCH];                      // active child LB2 (max over pairs)
   int16_t act[G::MAXCH];                  // child -> active slot, -1 if decided in B1
+  int16_t alist[G::MAXCH];                // B2 rounds: active slots still below best
   u64 bits[G::NWORDS + kBlock / kWave];
   int wpre[kBlock];
   int scan[kBlock / kWave];
@@ -580,6 +582,70 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     // ---- B2: (pair, child) Johnson walks, pair-major ----
     if (nact > 0 && a.lb2_wave) {
       lb2_walks_wave<NJ, M>(a, sm, __builtin_amdgcn_readfirstlane(nact), best);
+    } else if (nact > 0 && a.lb2_rounds) {
+      // Rounds of 8, 16, 32, ... pairs (learned early-exit order: the first pairs
+      // prune most children). Between rounds the children whose LB2 already exceeds
+      // best are dropped from the task list, so a wave's lanes no longer idle on
+      // skipped tasks; a round's tasks are dense (pair-major, consecutive lanes
+      // share the pair's records).
+      constexpr int PER = (G::MAXCH + kBlock - 1) / kBlock;
+      for (int i = tid; i < nact; i += kBlock) sm.alist[i] = static_cast<int16_t>(i);
+      __syncthreads();
+      int na = nact, q0 = 0, R = 8;
+      while (q0 < P && na > 0) {
+        const int nq = min(P - q0, R);
+        int qq = tid / na, ii = tid - (tid / na) * na;
+        const int dq = kBlock / na, di = kBlock - dq * na;
+        while (qq < nq) {
+          const int ai = sm.alist[ii];
+          if (sm.lbv[ai] <= best) {
+            const uint2 pi = sm.pinfo[q0 + qq];
+            int t0 = sm.cf[pi.x & 0xff][ai], t1 = sm.cf[(pi.x >> 8) & 0xff][ai];
+            u64 msk[G::NW];
+#pragma unroll
+            for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
+            const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
+#pragma unroll 4
+            for (int r = 0; r < N; ++r) {
+              const uint2 rc = rq[r];
+              const int n0 = t0 + static_cast<int>(rc.x >> 16);
+              const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
+              const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
+              t0 = sched ? t0 : n0;
+              t1 = sched ? t1 : n1;
+            }
+            atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
+          }
+          ii += di;
+          qq += dq;
+          if (ii >= na) {
+            ii -= na;
+            ++qq;
+          }
+        }
+        q0 += nq;
+        R *= 2;
+        __syncthreads();  // the round's LB2 maxima are final
+        if (q0 >= P) break;
+        int ent[PER];
+        bool kp[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          const int i = k * kBlock + tid;
+          ent[k] = i < na ? sm.alist[i] : -1;
+          kp[k] = ent[k] >= 0 && sm.lbv[ent[k]] <= best;
+        }
+        int nn = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {  // the scan's first barrier orders the reads above before the writes
+          int c = 0;
+          const int pos = nn + block_exclusive_scan(kp[k] ? 1 : 0, sm.scan, &c);
+          if (kp[k]) sm.alist[pos] = static_cast<int16_t>(ent[k]);
+          nn += c;
+        }
+        __syncthreads();
+        na = nn;
+      }
     } else if (nact > 0) {
       int q = tid / nact, ai = tid - (tid / nact) * nact;
       const int dq = kBlock / nact, da = kBlock - dq * nact;
