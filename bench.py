@@ -68,7 +68,7 @@ def main() -> int:
     golden = GOLDEN.get((a.inst, a.lb)) if a.ub == 1 else None
 
     def step():
-        r = distributed_solve(model, engine, comm, ub=a.ub, cfg=cfg)
+        r = distributed_solve(model, engine, comm, ub=a.ub, cfg=cfg, window=a.max_parents)
         if golden and (r.tree, r.sol, r.best) != golden:
             raise SystemExit(f"wrong result {(r.tree, r.sol, r.best)} != golden {golden}")
         return r

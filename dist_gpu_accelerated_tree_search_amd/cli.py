@@ -1,6 +1,6 @@
 """Command line (parity with the reference executables' flags, defaults and output).
 
-    python -m dist_gpu_accelerated_tree_search_amd pfsp  [-i 14 -l 1 -u 1 -m 25 -M 50000 -T 5000 -D 1 -C 0 -w 1 -L 1 -p 50]
+    python -m dist_gpu_accelerated_tree_search_amd pfsp  [-i 14 -l 1 -u 1 -m 25 -M 50000 -T 5000 -D 1 -C 1 -w 1 -L 1 -p 50]
     python -m dist_gpu_accelerated_tree_search_amd nqueens [-N 14 -g 1 -m 25 -M 50000 -D 1]
 
 pfsp:  -D 0            CPU only: -C threads (0/1 = sequential, ref pfsp_c / pfsp_omp_c)
@@ -37,7 +37,7 @@ def _pfsp_parser() -> argparse.ArgumentParser:
     ap.add_argument("-M", "--M", type=int, default=50000)
     ap.add_argument("-T", "--T", type=int, default=5000)
     ap.add_argument("-D", "--D", type=int, default=1)
-    ap.add_argument("-C", "--C", type=int, default=0)
+    ap.add_argument("-C", "--C", type=int, default=1)  # ref PFSP_lib.c:182 (*C = 1)
     ap.add_argument("-w", "--ws", type=int, default=1)
     ap.add_argument("-L", "--L", type=int, default=1)
     ap.add_argument("-p", "--perc", type=int, default=50)
@@ -205,7 +205,7 @@ def pfsp_main(argv: list[str]) -> int:
         # one process per GPU = the reference's distributed driver layout (one GPU per rank)
         report.write_dist_multi_gpu_csv(os.path.join(a.csv_dir, "dist_multigpu.csv"), a.inst, a.lb, 1, 0, a.L, D,
                                         res["best"], a.m, a.M, a.T, res["elapsed"], res["tree"], res["sol"], workers,
-                                        [w.steals for w in workers], [w.t_pool_ops for w in workers])
+                                        [w.dist_load_bal for w in workers], [w.t_load_bal for w in workers])
     if a.json:
         report.write_json_record(a.json, {**model.describe(), "n_gpus": D, "tree": res["tree"], "sol": res["sol"],
                                            "best": res["best"], "elapsed": res["elapsed"],

@@ -59,7 +59,7 @@ int main(int argc, char* argv[]) {
     constexpr int NJ = decltype(nj)::value;
     using Node = PfspNode<NJ>;
     if (cpu_threads > 0)
-      owned.push_back(std::make_unique<CpuEngine<PfspProblem<NJ>>>(PfspProblem<NJ>(in, host_lb), 4096, cpu_threads));
+      owned.push_back(std::make_unique<CpuEngine<PfspProblem<NJ>>>(PfspProblem<NJ>(in, host_lb), a.T, cpu_threads));
     std::vector<IEngine*> engines;
     for (auto& e : owned) engines.push_back(e.get());
     const int W = static_cast<int>(engines.size());
@@ -86,6 +86,15 @@ int main(int argc, char* argv[]) {
     rc.m = a.m;
     rc.steal_cap = static_cast<size_t>(5) * a.M;
     rc.work_sharing = a.ws == 1;
+    // GPU workers: needy below a quarter of the parent window, donors from one
+    // window; the CPU worker: the reference's m / 2m, at most 4*T per steal
+    for (auto* e : engines) {
+      const bool gpu = e->device() >= 0;
+      const size_t nb = gpu ? std::max<size_t>(a.m, max_parents / 4) : static_cast<size_t>(a.m);
+      rc.needy_below.push_back(nb);
+      rc.donor_min.push_back(gpu ? std::max(2 * nb, max_parents) : 2 * nb);
+      rc.recv_cap.push_back(gpu ? rc.steal_cap : std::min<size_t>(rc.steal_cap, static_cast<size_t>(4) * a.T));
+    }
     rc.merge_env();
     for (auto* e : engines) rc.worker_cpus.push_back(e->device() >= 0 ? device_cpus(e->device()) : std::vector<int>{});
     HipStaging staging;
@@ -97,8 +106,10 @@ int main(int argc, char* argv[]) {
       ws[w].tree = rep[w].st.tree;
       ws[w].sol = rep[w].st.sol;
       ws[w].gen_child = rep[w].st.tree;
-      ws[w].steals = ws[w].success_steals = rep[w].transfers_in;
-      ws[w].terminations = rep[w].rounds;
+      ws[w].steals = rep[w].steals;
+      ws[w].success_steals = rep[w].success_steals;
+      ws[w].terminations = rep[w].idle_rounds;
+      ws[w].t_termination = rep[w].t_termination;
       ws[w].t_memcpy = rep[w].st.t_memcpy;
       ws[w].t_malloc = rep[w].st.t_malloc;
       ws[w].t_kernel = rep[w].t_run;

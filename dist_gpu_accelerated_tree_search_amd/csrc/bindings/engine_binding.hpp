@@ -13,8 +13,10 @@
 #include <vector>
 #include <stdexcept>
 
+#include "../core/dist_rounds.hpp"
 #include "../core/engine_api.hpp"
 #include "../core/runner.hpp"
+#include "../core/shm_control.hpp"
 
 namespace py = pybind11;
 
@@ -37,6 +39,9 @@ inline py::dict engine_stats_dict(const EngineStats& s) {
   d["device_nodes"] = s.device_nodes;
   d["host_nodes"] = s.host_nodes;
   d["capacity"] = s.capacity;
+  d["exports"] = s.exports;
+  d["imports"] = s.imports;
+  d["pinned_bytes"] = s.pinned_bytes;
   return d;
 }
 
@@ -106,7 +111,157 @@ inline void bind_engine(py::module_& m) {
       .def_property("best", &IEngine::best, &IEngine::set_best)
       .def("reset_counters", &IEngine::reset_counters)
       .def("stats", [](IEngine& e) { return engine_stats_dict(e.stats()); })
-      .def("synchronize", &IEngine::synchronize, py::call_guard<py::gil_scoped_release>());
+      .def("synchronize", &IEngine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("transfer_stream", &IEngine::transfer_stream,
+                             "Stream on which work-sharing sends/receives are enqueued (0: host engine).")
+      .def("fence", &IEngine::fence, py::call_guard<py::gil_scoped_release>(),
+           "Wait on the host for every copy enqueued so far.");
+}
+
+// Intra-node control plane (csrc/core/shm_control.hpp), bound in both modules so the
+// native round loop of either one can use it (dist_rounds takes its address).
+inline void bind_shm_control(py::module_& m) {
+  using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+  py::class_<ShmControl>(m, "ShmControl", py::module_local())
+      .def(py::init<const std::string&, int, int, bool>(), py::arg("name"), py::arg("rank"), py::arg("world"),
+           py::arg("create"))
+      .def_property_readonly("rank", &ShmControl::rank)
+      .def_property_readonly("world", &ShmControl::world)
+      .def_property_readonly("rounds", &ShmControl::rounds)
+      .def_property_readonly("address", &ShmControl::address)
+      .def("unlink", &ShmControl::unlink)
+      .def(
+          "allgather",
+          [](ShmControl& c, I64 vals, double timeout_s) {
+            if (vals.ndim() != 1) throw std::invalid_argument("allgather: 1-D int64 values");
+            const int n = static_cast<int>(vals.shape(0));
+            I64 out({static_cast<py::ssize_t>(c.world()), static_cast<py::ssize_t>(n)});
+            const int64_t* src = vals.data();
+            int64_t* dst = out.mutable_data();
+            {
+              py::gil_scoped_release nogil;
+              c.allgather(src, n, dst, timeout_s);
+            }
+            return out;
+          },
+          py::arg("values"), py::arg("timeout_s") = 600.0,
+          "Collective all-gather of up to 15 int64 per rank -> (world, n) array.")
+      .def(
+          "barrier",
+          [](ShmControl& c, double timeout_s) {
+            py::gil_scoped_release nogil;
+            c.barrier(timeout_s);
+          },
+          py::arg("timeout_s") = 600.0)
+      .def("offer_best", &ShmControl::offer_best, py::arg("best"))
+      .def_property_readonly("best", &ShmControl::best)
+      .def("publish_size", &ShmControl::publish_size)
+      .def("peer_size", &ShmControl::peer_size)
+      .def("request_round", &ShmControl::request_round)
+      .def_property_readonly("round_requested", &ShmControl::round_requested);
+}
+
+// dist_rounds(engine, shm_address | allgather_fn, rank, world, options, transfer_fn,
+//             round_hook, rounds0, timeout_s) -> dict (core/dist_rounds.hpp)
+inline void bind_dist_rounds(py::module_& m) {
+  using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+  m.def(
+      "plan_transfers",
+      [](std::vector<int64_t> sizes, size_t needy_below, size_t donor_min, size_t cap, int local_world, bool intra,
+         bool inter) {
+        py::list out;
+        for (const auto& t : plan_transfers(sizes, needy_below, donor_min, cap, local_world, intra, inter))
+          out.append(py::make_tuple(t.donor, t.receiver, t.n));
+        return out;
+      },
+      py::arg("sizes"), py::arg("needy_below"), py::arg("donor_min"), py::arg("cap"), py::arg("local_world") = 0,
+      py::arg("intra") = true, py::arg("inter") = true);
+  m.def(
+      "dist_rounds",
+      [](IEngine& e, uintptr_t shm_address, py::object allgather_fn, int rank, int world, py::dict o,
+         py::object transfer_fn, py::object round_hook, unsigned long long rounds0, double timeout_s) {
+        DistOptions opt;
+        auto get = [&](const char* k, auto& v) {
+          if (o.contains(k)) v = o[k].cast<std::remove_reference_t<decltype(v)>>();
+        };
+        get("needy_below", opt.needy_below);
+        get("donor_min", opt.donor_min);
+        get("steal_cap", opt.steal_cap);
+        get("slice_min", opt.slice_min);
+        get("slice_max", opt.slice_max);
+        get("intra", opt.intra);
+        get("inter", opt.inter);
+        get("local_world", opt.local_world);
+        get("early_rounds", opt.early_rounds);
+        get("max_rounds", opt.max_rounds);
+        get("checkpoint_every", opt.checkpoint_every);
+        get("watchdog_s", opt.watchdog_s);
+        get("watchdog_abort", opt.watchdog_abort);
+        get("fault_delay_us", opt.fault_delay_us);
+        get("fault_steal_fail_pct", opt.fault_steal_fail_pct);
+        get("fault_seed", opt.fault_seed);
+        std::unique_ptr<RoundControl> ctl;
+        if (shm_address) {
+          ctl = std::make_unique<ShmRoundControl>(reinterpret_cast<ShmControl*>(shm_address), timeout_s);
+        } else {
+          if (allgather_fn.is_none()) throw std::invalid_argument("dist_rounds: give a shm address or an allgather_fn");
+          ctl = std::make_unique<FnRoundControl>(rank, world, [allgather_fn, world](const int64_t* v, int n, int64_t* out) {
+            py::gil_scoped_acquire gil;
+            I64 a(static_cast<py::ssize_t>(n));
+            std::memcpy(a.mutable_data(), v, sizeof(int64_t) * static_cast<size_t>(n));
+            I64 r = allgather_fn(a).cast<I64>();
+            if (r.size() != static_cast<py::ssize_t>(world) * n) throw std::runtime_error("allgather_fn: wrong shape");
+            std::memcpy(out, r.data(), sizeof(int64_t) * static_cast<size_t>(world) * static_cast<size_t>(n));
+          });
+        }
+        if (ctl->rank() != rank || ctl->world() != world) throw std::invalid_argument("dist_rounds: rank/world mismatch");
+        TransferFn xfer = [transfer_fn](const Plan& p) -> std::pair<size_t, size_t> {
+          py::gil_scoped_acquire gil;
+          py::list l;
+          for (const auto& t : p) l.append(py::make_tuple(t.donor, t.receiver, t.n));
+          py::tuple r = transfer_fn(l).cast<py::tuple>();
+          return {r[0].cast<size_t>(), r[1].cast<size_t>()};
+        };
+        RoundHook hook;
+        if (!round_hook.is_none())
+          hook = [round_hook](unsigned long long r, int b, bool rep) {
+            py::gil_scoped_acquire gil;
+            round_hook(r, b, rep);
+          };
+        DistOutcome out;
+        {
+          py::gil_scoped_release nogil;
+          out = run_dist_rounds(e, *ctl, opt, xfer, hook, rounds0);
+        }
+        py::dict d;
+        d["best"] = out.best;
+        d["complete"] = out.complete;
+        d["rounds"] = out.rounds;
+        d["watchdog_events"] = out.watchdog_events;
+        d["tree"] = out.tree;
+        d["sol"] = out.sol;
+        d["sent"] = out.sent;
+        d["received"] = out.received;
+        d["transfers_in"] = out.transfers_in;
+        d["transfers_out"] = out.transfers_out;
+        d["steals"] = out.steals;
+        d["success_steals"] = out.success_steals;
+        d["idle_rounds"] = out.idle_rounds;
+        d["early_rounds"] = out.early_rounds;
+        d["dropped"] = out.dropped;
+        d["t_run"] = out.t_run;
+        d["t_comm"] = out.t_comm;
+        d["t_idle"] = out.t_idle;
+        d["t_termination"] = out.t_termination;
+        d["t_load_bal"] = out.t_load_bal;
+        d["t_memcpy"] = out.t_memcpy;
+        d["t_malloc"] = out.t_malloc;
+        return d;
+      },
+      py::arg("engine"), py::arg("shm_address"), py::arg("allgather_fn"), py::arg("rank"), py::arg("world"),
+      py::arg("options"), py::arg("transfer_fn"), py::arg("round_hook") = py::none(), py::arg("rounds0") = 0,
+      py::arg("timeout_s") = 1800.0,
+      "Native lock-step rounds of a multi-rank solve until every pool is empty (or max_rounds).");
 }
 
 // run_workers(engines, initial_nodes, best, ...) -> {"best": int, "workers": [dict]}
@@ -121,7 +276,8 @@ inline void bind_runner(py::module_& m, StagingFactory staging = {}, CpusOfDevic
       "run_workers",
       [staging, cpus_of_device](py::list engines, py::list initial, int best, size_t m_, size_t steal_cap,
                                 double slice_min, double slice_max, bool ws, bool pin, bool device_steals,
-                                double watchdog_s, py::dict faults) {
+                                double watchdog_s, py::dict faults, std::vector<size_t> needy_below,
+                                std::vector<size_t> donor_min, std::vector<size_t> recv_cap) {
         if (engines.size() != initial.size()) throw std::invalid_argument("one initial node array per engine");
         std::vector<IEngine*> es;
         std::vector<std::vector<uint8_t>> init;
@@ -140,6 +296,9 @@ inline void bind_runner(py::module_& m, StagingFactory staging = {}, CpusOfDevic
         cfg.slice_max = slice_max;
         cfg.work_sharing = ws;
         cfg.watchdog_s = watchdog_s;
+        cfg.needy_below = std::move(needy_below);
+        cfg.donor_min = std::move(donor_min);
+        cfg.recv_cap = std::move(recv_cap);
         cfg.merge_env();
         if (faults.contains("delay_us")) cfg.fault_delay_us = faults["delay_us"].cast<unsigned>();
         if (faults.contains("steal_fail_pct")) cfg.fault_steal_fail_pct = faults["steal_fail_pct"].cast<unsigned>();
@@ -170,6 +329,10 @@ inline void bind_runner(py::module_& m, StagingFactory staging = {}, CpusOfDevic
           d["t_run_w"] = r.t_run;
           d["t_comm"] = r.t_comm;
           d["t_idle"] = r.t_idle;
+          d["t_termination"] = r.t_termination;
+          d["steals"] = r.steals;
+          d["success_steals"] = r.success_steals;
+          d["idle_rounds"] = r.idle_rounds;
           ws_out.append(d);
         }
         py::dict out;
@@ -180,6 +343,8 @@ inline void bind_runner(py::module_& m, StagingFactory staging = {}, CpusOfDevic
       py::arg("engines"), py::arg("initial"), py::arg("best"), py::arg("m") = 25, py::arg("steal_cap") = 250000,
       py::arg("slice_min") = 0.0005, py::arg("slice_max") = 0.05, py::arg("ws") = true, py::arg("pin") = false,
       py::arg("device_steals") = true, py::arg("watchdog_s") = 0.0, py::arg("faults") = py::dict(),
+      py::arg("needy_below") = std::vector<size_t>{}, py::arg("donor_min") = std::vector<size_t>{},
+      py::arg("recv_cap") = std::vector<size_t>{},
       "Drive several engines (GPUs and/or CPU workers) from one process until all pools are empty.");
   m.def("parse_cpulist", &parse_cpulist);
   m.def("allowed_cpus", &allowed_cpus);

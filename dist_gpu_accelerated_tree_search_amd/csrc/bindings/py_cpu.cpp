@@ -233,38 +233,6 @@ PYBIND11_MODULE(_tts_cpu, m) {
       },
       py::arg("N"), py::arg("G") = 1, py::arg("batch") = 4096, py::arg("threads") = 1);
 
-  // ---- intra-node control plane (csrc/core/shm_control.hpp) ----
-  using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
-  py::class_<ShmControl>(m, "ShmControl")
-      .def(py::init<const std::string&, int, int, bool>(), py::arg("name"), py::arg("rank"), py::arg("world"),
-           py::arg("create"))
-      .def_property_readonly("rank", &ShmControl::rank)
-      .def_property_readonly("world", &ShmControl::world)
-      .def_property_readonly("rounds", &ShmControl::rounds)
-      .def("unlink", &ShmControl::unlink)
-      .def(
-          "allgather",
-          [](ShmControl& c, I64 vals, double timeout_s) {
-            if (vals.ndim() != 1) throw std::invalid_argument("allgather: 1-D int64 values");
-            const int n = static_cast<int>(vals.shape(0));
-            I64 out({static_cast<py::ssize_t>(c.world()), static_cast<py::ssize_t>(n)});
-            const int64_t* src = vals.data();
-            int64_t* dst = out.mutable_data();
-            {
-              py::gil_scoped_release nogil;
-              c.allgather(src, n, dst, timeout_s);
-            }
-            return out;
-          },
-          py::arg("values"), py::arg("timeout_s") = 600.0,
-          "Collective all-gather of up to 15 int64 per rank -> (world, n) array.")
-      .def(
-          "barrier",
-          [](ShmControl& c, double timeout_s) {
-            py::gil_scoped_release nogil;
-            c.barrier(timeout_s);
-          },
-          py::arg("timeout_s") = 600.0)
-      .def("offer_best", &ShmControl::offer_best, py::arg("best"))
-      .def_property_readonly("best", &ShmControl::best);
+  bind_shm_control(m);
+  bind_dist_rounds(m);
 }

@@ -41,6 +41,8 @@ EngineConfig make_cfg(int device, size_t max_parents, size_t ring_bytes, int ite
 PYBIND11_MODULE(_tts_hip, m) {
   m.doc() = "gfx950 (MI355X) device engines: device-resident pools, fused bound/prune/compact kernels, hipGraphs.";
   bind_engine(m);
+  bind_shm_control(m);
+  bind_dist_rounds(m);
   bind_runner(
       m, []() -> std::unique_ptr<DeviceStaging> { return std::make_unique<HipStaging>(); }, &device_cpus);
   if (!std::getenv("TTS_NO_ROCTX")) install_roctx_hooks();

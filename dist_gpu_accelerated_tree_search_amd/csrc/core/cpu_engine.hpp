@@ -59,11 +59,18 @@ class CpuEngine final : public IEngine {
   long run(long max_launches, double max_seconds, size_t stop_below) override {
     const double t0 = now_s();
     long launches = 0;
-    if (split_world_ > 1 && !split_done_) do_split();
+    if (split_world_ > 1 && !split_done_) {
+      do_split(t0, max_seconds);
+      if (!split_done_ && !pool_.empty()) {  // time slice over while still replicated
+        t_run_ += now_s() - t0;
+        return 0;
+      }
+    }
     std::vector<Node> parents(batch_);
     while (!pool_.empty() && pool_.size() >= std::max<size_t>(stop_below, 1)) {
       if (max_launches >= 0 && launches >= max_launches) break;
       if (max_seconds > 0 && now_s() - t0 >= max_seconds) break;
+      if (hook_ && hook_(pool_.size())) break;
       const size_t n = pool_.pop_back_bulk_free(1, batch_, parents.data(), 1);
       expand(parents.data(), n);
       parents_ += n;
@@ -92,6 +99,7 @@ class CpuEngine final : public IEngine {
     arm_min_ = std::max<size_t>(1, min_parents);
   }
   bool split_pending() override { return split_world_ > 1 && !split_done_; }
+  void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
   EngineStats solve_from(const void* nodes, size_t n, int best) override {
     begin(nodes, n, best);
     run(-1, 0.0, 0);
@@ -138,9 +146,10 @@ class CpuEngine final : public IEngine {
   // rank until the pool holds split_min_ nodes, then a strided 1/world share;
   // ranks != 0 drop the replicated counts. A tree that dies out first is left to
   // rank 0 (stats()).
-  void do_split() {
+  void do_split(double t0, double max_seconds) {
     std::vector<Node> level;
     while (!pool_.empty() && pool_.size() < split_min_) {
+      if (max_seconds > 0 && now_s() - t0 >= max_seconds) return;  // resumed by the next run()
       level.resize(pool_.size());
       const size_t n = pool_.pop_back_bulk_free(1, level.size(), level.data(), 1);
       expand(level.data(), n);
@@ -192,6 +201,7 @@ class CpuEngine final : public IEngine {
   int arm_world_ = 0, arm_rank_ = 0, split_world_ = 0, split_rank_ = 0;
   size_t arm_min_ = 1, split_min_ = 1;
   bool split_done_ = false;
+  ProgressHook hook_;
 };
 
 // CPU engine that keeps its PFSP instance alive (for callers that build the
@@ -213,6 +223,7 @@ class OwningCpuEngine final : public IEngine {
   size_t warm_split(int r, int w, size_t win, int p) override { return eng_.warm_split(r, w, win, p); }
   void set_split(int r, int w, size_t mp) override { eng_.set_split(r, w, mp); }
   bool split_pending() override { return eng_.split_pending(); }
+  void set_progress_hook(ProgressHook h) override { eng_.set_progress_hook(std::move(h)); }
   void set_best(int b) override { eng_.set_best(b); }
   int best() override { return eng_.best(); }
   void reset_counters() override { eng_.reset_counters(); }

@@ -5,8 +5,15 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 
 namespace tts {
+
+// Called by run() between two graph replays (nothing in flight) with the current
+// pool size; returning true ends run() early. The distributed runtime uses it to
+// publish its pool size on the node-wide board and to answer a peer's early
+// round request (core/dist_rounds.hpp).
+using ProgressHook = std::function<bool(size_t pool)>;
 
 struct EngineConfig {
   int device = 0;
@@ -27,7 +34,8 @@ struct EngineConfig {
 struct EngineStats {
   unsigned long long tree = 0, sol = 0, parents = 0, iters = 0;
   int best = 0;
-  unsigned long long launches = 0, syncs = 0, spilled = 0, refilled = 0;
+  unsigned long long launches = 0, syncs = 0, spilled = 0, refilled = 0, exports = 0, imports = 0;
+  size_t pinned_bytes = 0;  // pinned host spill blocks held
   double t_run = 0, t_memcpy = 0, t_malloc = 0;
   size_t device_nodes = 0, host_nodes = 0, capacity = 0;
 };
@@ -39,8 +47,18 @@ class IEngine {
   virtual size_t node_bytes() const = 0;
   virtual void push_host(const void* nodes, size_t n) = 0;
   virtual size_t pop_host(void* out, size_t max_n) = 0;
+  // Work-sharing transfers through a device staging buffer, stream-ordered without
+  // host synchronisation (GPU engines): export_device enqueues the copy of the
+  // oldest nodes into `dst` and makes the transfer stream (transfer_stream())
+  // wait for it; import_device makes the compute stream wait for the transfer
+  // stream, then appends the nodes. A send/recv enqueued on the transfer stream
+  // between the two is therefore ordered on both sides. fence() waits on the host
+  // for everything enqueued so far (used before a host-side handoff).
   virtual size_t export_device(void* dst, size_t max_n) = 0;
   virtual void import_device(const void* src, size_t n) = 0;
+  virtual uintptr_t transfer_stream() const { return 0; }
+  virtual void fence() {}
+  virtual void set_progress_hook(ProgressHook hook) { (void)hook; }
   virtual size_t size() = 0;
   // Replays expand graphs until the pool is empty, `max_launches` graphs were
   // launched (<0: unlimited), `max_seconds` elapsed (<=0: unlimited), or the pool

@@ -36,6 +36,7 @@
 #include <tuple>
 #include <vector>
 
+#include "dist_rounds.hpp"
 #include "engine_api.hpp"
 #include "topology.hpp"
 #include "trace.hpp"
@@ -43,8 +44,11 @@
 namespace tts {
 
 struct RunnerConfig {
-  size_t m = 25;               // needy below m nodes, donors need >= 2m
+  size_t m = 25;               // needy below m nodes, donors need >= 2m (unless set per worker)
   size_t steal_cap = 250000;   // ref 5*M
+  // per-worker thresholds (plan_transfers): GPU workers in units of their parent
+  // window, CPU workers the reference's m / 2m with a 4*T receive cap
+  std::vector<size_t> needy_below, donor_min, recv_cap;
   double slice_min = 0.0005;   // seconds of local search between rounds (adaptive)
   double slice_max = 0.05;
   bool work_sharing = true;    // ref -w
@@ -84,7 +88,8 @@ struct WorkerReport {
   EngineStats st;
   unsigned long long rounds = 0, sent = 0, received = 0, transfers_in = 0, transfers_out = 0;
   unsigned long long device_transfers = 0, dropped_transfers = 0, watchdog_events = 0;
-  double t_run = 0, t_comm = 0, t_idle = 0;
+  unsigned long long steals = 0, success_steals = 0, idle_rounds = 0;  // ref nbSteals / nbSSteals / nbTermination
+  double t_run = 0, t_comm = 0, t_idle = 0, t_termination = 0;
   bool pinned = false;
 };
 
@@ -95,32 +100,6 @@ class DeviceStaging {
   virtual void* alloc(int device, size_t bytes) = 0;
   virtual void release(int device, void* p) = 0;
 };
-
-// Deterministic steal-half matching (identical to parallel/comm.py::plan_sharing
-// with a single node).
-inline std::vector<std::tuple<int, int, size_t>> plan_sharing(const std::vector<size_t>& sizes, size_t m,
-                                                              size_t cap) {
-  const int n = static_cast<int>(sizes.size());
-  std::vector<size_t> left = sizes;
-  std::vector<char> needy(n, 0);
-  for (int r = 0; r < n; ++r) needy[r] = sizes[r] < m;
-  std::vector<std::tuple<int, int, size_t>> plan;
-  for (int r = 0; r < n; ++r) {
-    if (!needy[r]) continue;
-    int d = -1;
-    for (int x = 0; x < n; ++x) {
-      if (x == r || needy[x] || left[x] < 2 * m) continue;
-      if (d < 0 || left[x] > left[d]) d = x;
-    }
-    if (d < 0) continue;
-    const size_t k = std::min(left[d] / 2, cap);
-    if (k == 0) continue;
-    left[d] -= k;
-    left[r] += k;
-    plan.emplace_back(d, r, k);
-  }
-  return plan;
-}
 
 class RoundBarrier {
  public:
@@ -171,6 +150,13 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
   std::vector<void*> dbuf(W, nullptr);
   std::vector<size_t> dcap(W, 0), dcount(W, 0);
   std::vector<std::tuple<int, int, size_t>> plan;
+  auto per = [&](const std::vector<size_t>& v, size_t dflt) {
+    std::vector<size_t> out(W, dflt);
+    for (int x = 0; x < W && x < static_cast<int>(v.size()); ++x) out[x] = v[x];
+    return out;
+  };
+  const std::vector<size_t> needy = per(cfg.needy_below, cfg.m), donor = per(cfg.donor_min, 2 * cfg.m),
+                            rcap = per(cfg.recv_cap, cfg.steal_cap);
   bool done = false;
   int gbest = best;
   double slice = cfg.slice_min;
@@ -276,14 +262,15 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
         gbest = *std::min_element(bests.begin(), bests.end());
         size_t total = 0;
         bool starving = false;
-        for (size_t s : sizes) {
-          total += s;
-          starving |= s < cfg.m;
+        for (int x = 0; x < W; ++x) {
+          total += sizes[x];
+          starving |= sizes[x] < needy[x];
         }
         done = total == 0;
         plan.clear();
         if (!done && cfg.work_sharing && W > 1 && starving) {
-          plan = plan_sharing(sizes, cfg.m, cfg.steal_cap);
+          std::vector<int64_t> sz(sizes.begin(), sizes.end());
+          for (const auto& t : plan_transfers(sz, needy, donor, rcap)) plan.emplace_back(t.donor, t.receiver, t.n);
           if (cfg.fault_steal_fail_pct) {
             std::vector<std::tuple<int, int, size_t>> kept;
             for (auto& t : plan) {
@@ -302,8 +289,11 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
       beats[w].round.store(r.rounds, std::memory_order_relaxed);
       if (done) {
         r.t_comm += secs(t1, now());
+        r.t_termination += secs(t1, now());
         break;
       }
+      const bool needy_w = cfg.work_sharing && W > 1 && sizes[w] < needy[w];
+      if (needy_w) ++r.steals;
       if (gbest < bests[w]) guarded([&] { e->set_best(gbest); });
       if (!plan.empty()) {
         beat(w, Phase::Transfer);
@@ -325,6 +315,7 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
                 dcap[rc] = k * nb;
               }
               got = e->export_device(dbuf[rc], k);
+              e->fence();  // stream-ordered copy: done before the receiver's barrier
             });
             dcount[rc] = got;
             ++r.device_transfers;
@@ -356,10 +347,20 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
           r.received += in;
           ++r.transfers_in;
         }
+        if (needy_w) {
+          if (in)
+            ++r.success_steals;
+          else
+            ++r.idle_rounds;
+        }
         beat(w, Phase::Barrier);
         bar.wait();
       }
-      if (sizes[w] == 0) r.t_idle += secs(t0, now());
+      if (plan.empty() && needy_w) ++r.idle_rounds;
+      if (sizes[w] == 0) {
+        r.t_idle += secs(t0, now());
+        r.t_termination += secs(t1, now());
+      }
       r.t_comm += secs(t1, now());
     }
     beat(w, Phase::Done);

@@ -23,6 +23,13 @@
 // every rank to have posted round r+1, i.e. to have finished reading round r —
 // so two buffers are enough and no reset is ever needed. A rank that does not
 // arrive within the timeout raises (failure detection).
+//
+// Board (not collective): every rank publishes its live pool size after each
+// graph replay, and a rank that ran dry while a peer holds enough work to donate
+// requests the next round early (request_round). Ranks still searching see the
+// request between two replays and join the round at once instead of finishing
+// their time slice — the counterpart of the reference's immediate steal attempt
+// by an idle thread (ref pfsp_multigpu_cuda.c:343-404).
 #pragma once
 
 #include <fcntl.h>
@@ -44,13 +51,13 @@ namespace tts {
 class ShmControl {
  public:
   static constexpr int kMaxVals = 15;
-  static constexpr uint64_t kMagic = 0x7474735f63746c31ull;  // "tts_ctl1"
+  static constexpr uint64_t kMagic = 0x7474735f63746c32ull;  // "tts_ctl2"
 
   // create=true: make (or replace) the segment `name` (rank 0); otherwise open it.
   ShmControl(const std::string& name, int rank, int world, bool create) : name_(name), rank_(rank), world_(world) {
     if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("ShmControl: bad rank/world");
     if (name.empty() || name[0] != '/') throw std::invalid_argument("ShmControl: name must start with '/'");
-    bytes_ = sizeof(Header) + 2 * static_cast<size_t>(world) * sizeof(Slot);
+    bytes_ = sizeof(Header) + static_cast<size_t>(world) * sizeof(Board) + 2 * static_cast<size_t>(world) * sizeof(Slot);
     int fd = -1;
     if (create) {
       (void)shm_unlink(name.c_str());  // stale segment of a crashed run
@@ -76,7 +83,8 @@ class ShmControl {
     if (p == MAP_FAILED) throw std::runtime_error(std::string("mmap: ") + std::strerror(errno));
     base_ = static_cast<char*>(p);
     hdr_ = reinterpret_cast<Header*>(base_);
-    slots_ = reinterpret_cast<Slot*>(base_ + sizeof(Header));
+    board_ = reinterpret_cast<Board*>(base_ + sizeof(Header));
+    slots_ = reinterpret_cast<Slot*>(base_ + sizeof(Header) + static_cast<size_t>(world) * sizeof(Board));
     if (create) {
       std::memset(base_, 0, bytes_);  // ftruncate already zeroes; be explicit
       hdr_->world = world;
@@ -106,6 +114,11 @@ class ShmControl {
 
   // out[r * n + i] = value i of rank r. Collective: every rank calls it in the same order.
   void allgather(const int64_t* vals, int n, int64_t* out, double timeout_s) {
+    allgather(vals, n, out, timeout_s, [] {});
+  }
+  // Same, calling idle() now and then while waiting for the other ranks.
+  template <class Idle>
+  void allgather(const int64_t* vals, int n, int64_t* out, double timeout_s, Idle&& idle) {
     if (n < 0 || n > kMaxVals) throw std::invalid_argument("ShmControl::allgather: at most 15 values");
     const uint64_t r = ++round_;
     const int par = static_cast<int>(r & 1);
@@ -117,7 +130,8 @@ class ShmControl {
       Slot& s = slot(par, q);
       unsigned spins = 0;
       while (s.seq.load(std::memory_order_acquire) < r) {
-        if (++spins < 2048) {
+        if ((++spins & 63) == 0) idle();
+        if (spins < 2048) {
           __builtin_ia32_pause();
           continue;
         }
@@ -145,12 +159,34 @@ class ShmControl {
   }
   int64_t best() const { return hdr_->best.load(std::memory_order_acquire); }
 
+  // ---- board ----
+  void publish_size(int64_t n) { board_[rank_].size.store(n, std::memory_order_relaxed); }
+  int64_t peer_size(int r) const { return board_[r].size.load(std::memory_order_relaxed); }
+  // Ask every rank to join round `r` (the next all-gather) as soon as it can.
+  void request_round(uint64_t r) {
+    uint64_t cur = hdr_->request.load(std::memory_order_relaxed);
+    while (cur < r && !hdr_->request.compare_exchange_weak(cur, r, std::memory_order_acq_rel)) {
+    }
+  }
+  // Has a peer asked for an all-gather this rank has not joined yet?
+  bool round_requested() const { return hdr_->request.load(std::memory_order_acquire) > round_; }
+
+  // Object identity for a native caller built by the other compiler (the g++ and
+  // hipcc modules share this header): address + layout tag.
+  uintptr_t address() const { return reinterpret_cast<uintptr_t>(this); }
+  static uint64_t layout_tag() { return kMagic ^ (static_cast<uint64_t>(sizeof(ShmControl)) << 48); }
+  uint64_t tag() const { return tag_; }
+
  private:
   struct alignas(128) Header {
     std::atomic<uint64_t> magic;
     int world;
     int pad;
     std::atomic<int64_t> best;
+    std::atomic<uint64_t> request;  // highest all-gather round requested early
+  };
+  struct alignas(128) Board {
+    std::atomic<int64_t> size;  // live pool size of the rank
   };
   struct alignas(128) Slot {
     std::atomic<uint64_t> seq;
@@ -166,8 +202,10 @@ class ShmControl {
   size_t bytes_ = 0;
   char* base_ = nullptr;
   Header* hdr_ = nullptr;
+  Board* board_ = nullptr;
   Slot* slots_ = nullptr;
   uint64_t round_ = 0;
+  uint64_t tag_ = layout_tag();
 };
 
 }  // namespace tts

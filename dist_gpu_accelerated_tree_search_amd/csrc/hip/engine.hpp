@@ -8,9 +8,14 @@
 //   * K fused expand iterations captured once into a hipGraph and replayed; the
 //     iteration count, parent window and pool sizes live in device memory
 //     (PoolCtl), so the host only reads a 1-KB control block between replays,
-//   * host spill/refill of the ring bottom when the ring nears capacity, and
-//     bottom export/import for work sharing between GPUs (steal the shallowest,
-//     largest subtrees, RCCL transfer done by the caller: parallel/).
+//   * a pinned host extension of the ring bottom (host_spill.hpp): spills and
+//     refills are asynchronous DMA on a second (transfer) stream that overlap the
+//     graph replays; the ring span a copy touches stays reserved until its event
+//     completes, and refills are issued ahead of need (below 4 windows),
+//   * bottom export/import for work sharing between GPUs (steal the shallowest,
+//     largest subtrees): stream-ordered with events against the transfer stream,
+//     on which the caller enqueues the RCCL send/recv (parallel/comm.py), so no
+//     side waits on the host.
 #pragma once
 
 #include <algorithm>
@@ -22,6 +27,7 @@
 #include <vector>
 
 #include "../core/engine_api.hpp"
+#include "host_spill.hpp"
 #include "pool_device.hpp"
 
 namespace tts {
@@ -39,7 +45,8 @@ class DeviceEngine final : public IEngine {
   using Node = typename Traits::Node;
   using Args = typename Traits::Args;
 
-  DeviceEngine(const EngineConfig& cfg, const Args& problem_args) : cfg_(cfg), args_(problem_args) {
+  DeviceEngine(const EngineConfig& cfg, const Args& problem_args)
+      : cfg_(cfg), args_(problem_args), spill_(spill_block_nodes(cfg)) {
     if (cfg_.iters_small % 6 || cfg_.iters_large % 6 || cfg_.iters_small <= 0 || cfg_.iters_large <= 0)
       throw std::invalid_argument("iterations per graph must be positive multiples of 6");
     if (cfg_.max_parents == 0) throw std::invalid_argument("max_parents must be > 0");
@@ -70,6 +77,9 @@ class DeviceEngine final : public IEngine {
       TTS_HIP_CHECK(hipEventCreateWithFlags(&graph_done_[m], hipEventDisableTiming));
     }
     TTS_HIP_CHECK(hipEventCreateWithFlags(&up_done_, hipEventDisableTiming));
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_comp_, hipEventDisableTiming));
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_xfer_, hipEventDisableTiming));
+    TTS_HIP_CHECK(hipStreamCreateWithFlags(&xfer_, hipStreamNonBlocking));
     std::memset(h_ctl_, 0, sizeof(dev::PoolCtl));
     h_ctl_->best.v = 0x7fffffff;
     if (cfg_.external_stream) {
@@ -142,6 +152,8 @@ class DeviceEngine final : public IEngine {
   ~DeviceEngine() override {
     (void)hipSetDevice(cfg_.device);
     if (stream_) (void)hipStreamSynchronize(stream_);
+    if (xfer_) (void)hipStreamSynchronize(xfer_);
+    spill_.clear();
     for (auto& gs : graphs_)
       for (auto g : gs) (void)hipGraphExecDestroy(g);
     for (void* p : owned_) (void)hipFree(p);
@@ -159,11 +171,21 @@ class DeviceEngine final : public IEngine {
       (void)hipEventDestroy(graph_done_[m]);
     }
     (void)hipEventDestroy(up_done_);
+    (void)hipEventDestroy(ev_comp_);
+    (void)hipEventDestroy(ev_xfer_);
+    if (xfer_) (void)hipStreamDestroy(xfer_);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
   }
 
   size_t node_bytes() const override { return sizeof(Node); }
   uintptr_t stream() const override { return reinterpret_cast<uintptr_t>(stream_); }
+  uintptr_t transfer_stream() const override { return reinterpret_cast<uintptr_t>(xfer_); }
+  void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
+  void fence() override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    TTS_HIP_CHECK(hipStreamSynchronize(xfer_));
+  }
   int device() const override { return cfg_.device; }
   int grid() const { return grid_; }
   size_t max_parents() const { return cfg_.max_parents; }
@@ -173,30 +195,27 @@ class DeviceEngine final : public IEngine {
   void push_host(const void* nodes, size_t n) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     if (n == 0) return;
-    sync_ctl();
+    settle();
     normalize();
     const Node* src = static_cast<const Node*>(nodes);
-    // keep at least half the ring free for in-flight growth; the rest waits on the host
-    const size_t room = cap_ / 2 > dev_stack() ? cap_ / 2 - dev_stack() : 0;
+    // keep at least half the ring free for in-flight growth; the rest waits in the
+    // pinned spill (it joins the pool's bottom, DeviceEngine::run refills it)
+    const size_t used = dev_stack() + reserved_;
+    const size_t room = cap_ / 2 > used ? cap_ / 2 - used : 0;
     const size_t to_dev = std::min(n, room);
-    if (to_dev < n) spill_.insert(spill_.end(), src + to_dev, src + n);
+    if (to_dev < n) spill_.push_host(src + to_dev, n - to_dev);
     ring_write_top(src, to_dev, hipMemcpyHostToDevice);
     upload_ctl();
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
+  // Oldest nodes first: the pinned spill, then the ring bottom.
   size_t pop_host(void* out, size_t max_n) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
-    sync_ctl();
+    settle();
     normalize();
     Node* dst = static_cast<Node*>(out);
-    size_t got = 0;
-    const size_t from_spill = std::min(max_n, spill_.size());
-    if (from_spill) {
-      std::copy(spill_.end() - from_spill, spill_.end(), dst);
-      spill_.resize(spill_.size() - from_spill);
-      got += from_spill;
-    }
+    size_t got = spill_.pop_oldest(dst, max_n);
     const size_t from_dev = std::min(max_n - got, dev_stack());
     ring_read_bottom(dst + got, from_dev, hipMemcpyDeviceToHost);
     got += from_dev;
@@ -205,36 +224,46 @@ class DeviceEngine final : public IEngine {
     return got;
   }
 
+  // Stream-ordered (engine_api.hpp): no host wait unless spilled nodes must come back first.
   size_t export_device(void* dst, size_t max_n) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
-    sync_ctl();
+    settle();
     normalize();
-    refill(max_n);
+    while (dev_stack() < max_n && !spill_.empty()) {
+      if (!start_refill(max_n - dev_stack())) break;
+      finish_refill();
+    }
     const size_t n = std::min(max_n, dev_stack());
+    if (n == 0) return 0;
+    // the staging buffer may still be read by the previous send on the transfer stream
+    order(xfer_, stream_);
     ring_read_bottom(static_cast<Node*>(dst), n, hipMemcpyDeviceToDevice);
     upload_ctl();
-    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    order(stream_, xfer_);  // the send waits for the copy
+    ++stats_.exports;
     return n;
   }
 
   void import_device(const void* src, size_t n) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     if (n == 0) return;
-    sync_ctl();
+    settle();
     normalize();
-    if (dev_stack() + n > cap_ / 2) {
-      // make room on the device: spill the ring bottom first
-      spill_bottom(dev_stack() + n - cap_ / 2);
+    if (dev_stack() + reserved_ + n > cap_ / 2) {
+      // make room on the device: the ring bottom goes to the pinned spill
+      spill_bottom(dev_stack() + reserved_ + n - cap_ / 2);
     }
+    order(xfer_, stream_);  // the receive has landed
     ring_write_top(static_cast<const Node*>(src), n, hipMemcpyDeviceToDevice);
     upload_ctl();
-    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    order(stream_, xfer_);  // the next receive into the buffer waits for this copy
+    ++stats_.imports;
   }
 
   size_t size() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();
-    return dev_total() + spill_.size();
+    return dev_total() + spill_.size() + refill_n_;
   }
 
   long run(long max_launches, double max_seconds, size_t stop_below) override {
@@ -244,21 +273,42 @@ class DeviceEngine final : public IEngine {
     long launches = 0;
     sync_ctl();
     for (;;) {
-      // ---- nothing in flight: the host shadow is the device state ----
+      // ---- nothing in flight on the compute stream: the host shadow is the device state ----
       check_overflow();
+      poll_transfers();
       size_t total = dev_total();
-      if (total + spill_.size() == 0) break;
-      if (total + spill_.size() < stop_below) break;
+      const size_t all = total + spill_.size() + refill_n_;
+      if (all == 0) break;
+      if (all < stop_below) break;
       if (max_launches >= 0 && launches >= max_launches) break;
       if (max_seconds > 0 && elapsed() >= max_seconds) break;
-      if (total < cfg_.max_parents && !spill_.empty()) {  // refill from the host spill
+      if (hook_ && hook_(all)) break;
+      // refill ahead of need from the pinned spill (overlaps the next replays)
+      if (refill_n_ == 0 && !spill_.empty() && total < 4 * cfg_.max_parents) {
         normalize();
-        refill(cfg_.max_parents * 4);
+        start_refill(4 * cfg_.max_parents);
         upload_ctl();
         total = dev_total();
       }
+      if (total == 0) {  // the pool is all on the host: wait for a copy to land
+        if (refill_n_)
+          finish_refill();
+        else if (!resv_.empty())
+          TTS_HIP_CHECK(hipEventSynchronize(resv_.front().first));
+        else
+          throw std::runtime_error("pinned spill: no room on the device ring for a refill");
+        continue;
+      }
       int gi = pick_graph(total, 0);
       if (gi < 0) {
+        if (!resv_.empty()) {  // ring span still being copied out: wait for the oldest copy
+          TTS_HIP_CHECK(hipEventSynchronize(resv_.front().first));
+          continue;
+        }
+        if (refill_n_) {
+          finish_refill();
+          continue;
+        }
         normalize();
         spill_bottom(dev_stack() / 2 + 1);
         upload_ctl();
@@ -296,7 +346,7 @@ class DeviceEngine final : public IEngine {
   // ring base, one asynchronous control upload (no stream synchronisation).
   void begin(const void* nodes, size_t n, int best) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
-    sync_ctl();
+    settle();
     normalize();
     // an armed split applies to this solve only
     h_ctl_->split_world = arm_world_ > 1 ? arm_world_ : 0;
@@ -307,7 +357,7 @@ class DeviceEngine final : public IEngine {
     arm_world_ = 0;
     if (armed && n > cfg_.max_parents)
       throw std::invalid_argument("set_split: begin() with more nodes than the parent window");
-    if (dev_total() != 0 || !spill_.empty() || n > cap_ / 2) {
+    if (dev_total() != 0 || !spill_.empty() || reserved_ || n > cap_ / 2) {
       reset_counters();
       set_best(best);
       push_host(nodes, n);
@@ -336,7 +386,7 @@ class DeviceEngine final : public IEngine {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
     const auto t0 = std::chrono::steady_clock::now();
-    sync_ctl();
+    settle();
     // 6-iteration passes with a narrower parent window (plain launches: the
     // window is a kernel argument); identical on every rank
     const size_t win = std::max<size_t>(1, std::min(window, cfg_.max_parents));
@@ -381,11 +431,7 @@ class DeviceEngine final : public IEngine {
       }
       h_ctl_->bot = 0;
       h_ctl_->slot[0].stack = keep;
-      if (!spill_.empty()) {
-        std::vector<Node> mine;
-        for (size_t i = rank; i < spill_.size(); i += world) mine.push_back(spill_[i]);
-        spill_.swap(mine);
-      }
+      if (!spill_.empty()) spill_.keep_strided(rank, world);
       if (rank != 0) h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
       upload_ctl();
     }
@@ -435,14 +481,15 @@ class DeviceEngine final : public IEngine {
     s.tree = h_ctl_->tree + h_ctl_->pend_children + h_ctl_->pend_internal;
     s.sol = h_ctl_->sol + h_ctl_->pend_leaves;
     if (h_ctl_->split_world > 1 && !h_ctl_->slot[0].sdone && h_ctl_->split_rank != 0 && dev_total() == 0 &&
-        spill_.empty())
+        spill_.empty() && refill_n_ == 0)
       s.tree = s.sol = 0;  // the tree died out before the split: every rank explored all of it
     s.parents = h_ctl_->parents;
     s.iters = h_ctl_->iters;
     s.best = h_ctl_->best.v;
     s.device_nodes = dev_total();
-    s.host_nodes = spill_.size();
+    s.host_nodes = spill_.size() + refill_n_;
     s.capacity = cap_;
+    s.pinned_bytes = spill_.pinned_bytes();
     return s;
   }
   void synchronize() override {
@@ -510,7 +557,7 @@ class DeviceEngine final : public IEngine {
     while (want < static_cast<size_t>(cfg_.iters_large) && total >= (want / 6) * 2 * cfg_.max_parents) want *= 2;
     for (int i = static_cast<int>(ks_.size()) - 1; i >= 0; --i) {
       if (static_cast<size_t>(ks_[i]) > want && i > 0) continue;
-      if (total + extra + static_cast<size_t>(ks_[i] + 1) * buf_nodes_ <= cap_) return i;
+      if (total + extra + reserved_ + static_cast<size_t>(ks_[i] + 1) * buf_nodes_ <= cap_) return i;
     }
     return -1;
   }
@@ -566,28 +613,89 @@ class DeviceEngine final : public IEngine {
     h_ctl_->slot[0].stack -= n;
   }
 
+  // Pinned spill blocks: 1/16 of the ring, between 64K nodes and 256 MB.
+  static size_t spill_block_nodes(const EngineConfig& c) {
+    const size_t by_ring = c.ring_bytes / 16 / sizeof(Node);
+    const size_t cap = (size_t(256) << 20) / sizeof(Node);
+    return std::max<size_t>(size_t(1) << 16, std::min(by_ring, cap));
+  }
+  // `after` waits for everything enqueued on `before` so far (no host wait).
+  void order(hipStream_t before, hipStream_t after) {
+    hipEvent_t ev = before == stream_ ? ev_comp_ : ev_xfer_;
+    TTS_HIP_CHECK(hipEventRecord(ev, before));
+    TTS_HIP_CHECK(hipStreamWaitEvent(after, ev, 0));
+  }
+  // Host shadow current and every asynchronous spill copy folded in.
+  void settle() {
+    sync_ctl();
+    if (refill_n_) finish_refill();
+    poll_transfers();
+  }
+  // Release the ring span of spill copies that have completed; fold a completed
+  // refill (host shadow current, i.e. nothing in flight on the compute stream).
+  void poll_transfers() {
+    while (!resv_.empty()) {
+      const hipError_t q = hipEventQuery(resv_.front().first);
+      if (q == hipErrorNotReady) break;
+      TTS_HIP_CHECK(q);
+      reserved_ -= resv_.front().second;
+      resv_.pop_front();
+    }
+    if (refill_n_) {
+      const hipError_t q = hipEventQuery(refill_ev_);
+      if (q == hipSuccess)
+        fold_refill();
+      else if (q != hipErrorNotReady)
+        TTS_HIP_CHECK(q);
+    }
+  }
+  // Asynchronous D2H of the n oldest ring nodes into the pinned spill, on the
+  // transfer stream; the ring span stays reserved until the copy has completed.
   void spill_bottom(size_t n) {
     n = std::min(n, dev_stack());
     if (n == 0) return;
-    const size_t old = spill_.size();
-    spill_.resize(old + n);
-    // oldest device nodes go to the end of the host spill (taken first on refill)
-    std::vector<Node> tmp(n);
-    ring_read_bottom(tmp.data(), n, hipMemcpyDeviceToHost);
-    std::copy(tmp.begin(), tmp.end(), spill_.begin() + old);
+    order(stream_, xfer_);  // the nodes were written by earlier replays
+    const size_t start = h_ctl_->bot & (cap_ - 1);
+    const size_t first = std::min(n, cap_ - start);
+    auto reserve = [&](hipEvent_t ev, size_t k) {
+      resv_.emplace_back(ev, k);
+      reserved_ += k;
+    };
+    spill_.push_from_device(d_ring_ + start, first, xfer_, reserve);
+    if (first < n) spill_.push_from_device(d_ring_, n - first, xfer_, reserve);
+    h_ctl_->bot = (h_ctl_->bot + n) & (cap_ - 1);
+    h_ctl_->slot[0].stack -= n;
     stats_.spilled += n;
   }
-
-  void refill(size_t want) {
-    const size_t n = std::min(want, spill_.size());
-    if (n == 0) return;
-    const size_t room = cap_ / 2 > dev_stack() ? cap_ / 2 - dev_stack() : 0;
-    const size_t m = std::min(n, room);
-    if (m == 0) return;
-    ring_write_top(spill_.data() + (spill_.size() - m), m, hipMemcpyHostToDevice);
-    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
-    spill_.resize(spill_.size() - m);
-    stats_.refilled += m;
+  // Asynchronous H2D of up to `want` of the newest spilled nodes under the ring
+  // bottom (one pinned block at most), on the transfer stream. The nodes join the
+  // pool when the copy has completed (fold_refill). Returns false without room.
+  bool start_refill(size_t want) {
+    if (refill_n_ || spill_.empty() || want == 0) return false;
+    const size_t used = dev_total() + reserved_ + static_cast<size_t>(ks_.back() + 1) * buf_nodes_;
+    if (used >= cap_) return false;
+    const size_t b0 = h_ctl_->bot & (cap_ - 1);
+    size_t k = std::min({want, spill_.size(), cap_ - used, b0 ? b0 : cap_});
+    Node* dst = d_ring_ + ((b0 + cap_ - k) & (cap_ - 1));
+    k = spill_.pop_to_device(dst, k, xfer_, &refill_ev_);
+    if (k == 0) return false;
+    refill_n_ = k;
+    reserved_ += k;
+    return true;
+  }
+  void finish_refill() {
+    if (!refill_n_) return;
+    TTS_HIP_CHECK(hipEventSynchronize(refill_ev_));
+    fold_refill();
+  }
+  void fold_refill() {
+    TTS_HIP_CHECK(hipStreamWaitEvent(stream_, refill_ev_, 0));
+    h_ctl_->bot = (h_ctl_->bot + cap_ - refill_n_) & (cap_ - 1);
+    h_ctl_->slot[0].stack += refill_n_;
+    reserved_ -= refill_n_;
+    stats_.refilled += refill_n_;
+    refill_n_ = 0;
+    upload_ctl();
   }
 
   void launch_graph(int gi) {
@@ -645,6 +753,13 @@ class DeviceEngine final : public IEngine {
   dev::PoolCtl* d_mirror_[2] = {nullptr, nullptr};
   hipEvent_t graph_done_[2] = {nullptr, nullptr};
   hipEvent_t up_done_ = nullptr;
+  hipEvent_t ev_comp_ = nullptr, ev_xfer_ = nullptr;  // stream ordering (order())
+  hipStream_t xfer_ = nullptr;                         // spills, refills, work-sharing sends/receives
+  std::deque<std::pair<hipEvent_t, size_t>> resv_;     // spill copies in flight (ring span reserved)
+  size_t reserved_ = 0;                                // ring nodes reserved by copies in flight
+  size_t refill_n_ = 0;                                // nodes of the refill in flight
+  hipEvent_t refill_ev_ = nullptr;
+  ProgressHook hook_;
   int next_mirror_ = 0;
   std::deque<int> inflight_, inflight_k_;
   std::deque<dev::u64> inflight_seq_;
@@ -657,7 +772,7 @@ class DeviceEngine final : public IEngine {
   std::vector<int> ks_;
   std::vector<hipGraphExec_t> graphs_[2];
   std::vector<void*> owned_;
-  std::vector<Node> spill_;
+  PinnedSpill<Node> spill_;
   EngineStats stats_;
 };
 

@@ -43,6 +43,15 @@ def save(directory: str, rank: int, world: int, model, engine, tree: int, sol: i
     return path
 
 
+def prune(directory: str, keep_world: int) -> None:
+    """Remove checkpoint files of other world sizes (after every rank of the current
+    world has written its file), so a later resume never sees mixed worlds."""
+    for f in glob.glob(os.path.join(directory, "ckpt_rank*_of*.npz")):
+        w = int(os.path.basename(f).split("_of")[1].split(".")[0])
+        if w != keep_world:
+            os.remove(f)
+
+
 def load_all(directory: str, model) -> tuple[np.ndarray, int, int, int, int]:
     """All saved pools (concatenated in rank order) + summed counters, min incumbent,
     max rounds. Validates that the checkpoint belongs to `model`."""

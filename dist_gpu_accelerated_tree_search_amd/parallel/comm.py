@@ -10,7 +10,10 @@ transfer issued by all ranks in the same order:
                       Allreduce(best) + Allgather(termination) + Allgather(needs)
   * work transfer     batch_isend_irecv donor -> needy only, straight from the
                       device pool (engine.export_to) into the peer's pool over xGMI;
-                      never an all-gather of everybody's nodes.
+                      never an all-gather of everybody's nodes. Stream-ordered:
+                      the copy out of the pool, the RCCL send/recv (on the
+                      engine's transfer stream) and the copy into the peer's pool
+                      are chained with events, without a host wait.
   * final reduction   all_reduce SUM of counters / MIN of the incumbent.
 When every rank is on this node (torchrun --nnodes=1) the status records, barriers
 and final reductions go through a shared-memory control plane instead
@@ -85,10 +88,37 @@ class Comm:
         self._buf = None
         self.bytes_sent = 0
         self.bytes_recv = 0
+        self.device_transfers = 0   # transfers through device staging (GPU engines)
+        self.host_transfers = 0     # transfers through host arrays (CPU engines)
         self.timeout_s = timeout_s
         self.ctl = None
+        self._staging = {}
         if shm_control_wanted(self.topo):
             self.ctl = self._open_shm_control()
+        if self.distributed and use_gpu and self.backend == "nccl":
+            self._connect_peers()
+
+    def _connect_peers(self) -> None:
+        """RCCL sets up a point-to-point channel on first use; do it for every pair now
+        (one grouped send/recv of one byte per peer), outside any timed region."""
+        torch, dist = self.torch, self.dist
+        me, n = self.rank, self.world
+        send = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        recv = torch.empty(n, dtype=torch.uint8, device=self.device)
+        ops = []
+        for p in range(n):
+            if p != me:
+                ops.append(dist.P2POp(dist.isend, send[p:p + 1], p))
+                ops.append(dist.P2POp(dist.irecv, recv[p:p + 1], p))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        torch.cuda.synchronize(self.device)
+
+    def control_address(self, module) -> int:
+        """Address of this rank's shared-memory control plane for the native round loop
+        of `module` (the ShmControl object is shared by both native modules, same
+        header and layout), or 0 when rounds go through the process group."""
+        return int(self.ctl.address) if self.ctl is not None else 0
 
     def _open_shm_control(self):
         """Shared-memory control plane for a single-node job (csrc/core/shm_control.hpp):
@@ -201,19 +231,24 @@ class Comm:
         return out.cpu().numpy().reshape(self.world, vals.size)
 
     # ---- node transfers ----
-    def _buffer(self, nbytes: int):
-        if self._buf is None or self._buf.numel() < nbytes:
-            cap = max(nbytes, 1 << 20)
-            self._buf = self.torch.empty(cap, dtype=self.torch.uint8, device=self.device)
-        return self._buf
+    def _stage(self, device, nbytes: int, slot: str):
+        key = (str(device), slot)
+        buf = self._staging.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = self.torch.empty(max(nbytes, 1 << 20), dtype=self.torch.uint8, device=device)
+            self._staging[key] = buf
+        return buf
 
     def execute_transfers(self, plan, engine, node_bytes: int) -> tuple[int, int]:
         """Run the planned (donor, receiver, count) transfers. Every rank calls this
         with the same plan. Returns (nodes_sent, nodes_received) for this rank.
 
-        GPU comm (RCCL): nodes go device pool -> device buffer -> xGMI -> peer buffer
-        -> peer pool, never touching host memory. CPU comm (gloo): nodes are staged
-        through host arrays (this also lets GPU engines share one device in tests)."""
+        GPU engine + RCCL: pool -> device staging -> send/recv over xGMI -> peer
+        staging -> peer pool, every step enqueued on the engine's streams and
+        ordered by events (engine_api.hpp): no host wait, no device-wide sync.
+        GPU engine + gloo (ranks sharing a GPU in tests): the same device staging,
+        with a host hop around the gloo send/recv.
+        CPU engine: host arrays (engine.pop / engine.push)."""
         me = self.rank
         outgoing = [(r, k) for (d, r, k) in plan if d == me and k > 0]
         incoming = [(d, k) for (d, r, k) in plan if r == me and k > 0]
@@ -221,18 +256,34 @@ class Comm:
             return 0, 0
         total_out = sum(k for _, k in outgoing)
         total_in = sum(k for _, k in incoming)
-        torch = self.torch
-        on_device = self.device.type != "cpu"
-        ops = []
-        if on_device:
-            buf = self._buffer(max(total_out, total_in) * node_bytes)
-            if outgoing:
-                got = engine.export_to(buf.data_ptr(), total_out)
-                if got != total_out:
-                    raise RuntimeError(f"rank {me}: planned to send {total_out} nodes, pool gave {got}")
-            src = buf
-            dst = buf
+        torch, dist = self.torch, self.dist
+        xs = int(getattr(engine, "transfer_stream", 0) or 0)
+        if xs:
+            self.device_transfers += 1
+            dev = torch.device("cuda", engine.device)
+            stream = torch.cuda.ExternalStream(xs, device=dev)
+            nccl = self.backend == "nccl"
+            with torch.cuda.stream(stream):
+                src = dst = None
+                if outgoing:
+                    src = self._stage(dev, total_out * node_bytes, "out")
+                    got = engine.export_to(src.data_ptr(), total_out)
+                    if got != total_out:
+                        raise RuntimeError(f"rank {me}: planned to send {total_out} nodes, pool gave {got}")
+                    if not nccl:  # host hop (on the transfer stream, after the export copy)
+                        src = src[:total_out * node_bytes].cpu()
+                if incoming:
+                    dst = self._stage(dev, total_in * node_bytes, "in")
+                    if not nccl:
+                        dst_dev, dst = dst, torch.empty(total_in * node_bytes, dtype=torch.uint8)
+                self._p2p(outgoing, incoming, src, dst, node_bytes)
+                if incoming:
+                    if not nccl:
+                        dst_dev[:total_in * node_bytes].copy_(dst, non_blocking=False)
+                        dst = dst_dev
+                    engine.import_from(dst.data_ptr(), total_in)
         else:
+            self.host_transfers += 1
             src = None
             if outgoing:
                 host = engine.pop(total_out)
@@ -240,32 +291,38 @@ class Comm:
                     raise RuntimeError(f"rank {me}: planned to send {total_out} nodes, pool gave {len(host)}")
                 src = torch.from_numpy(np.ascontiguousarray(host).reshape(-1))
             dst = torch.empty(total_in * node_bytes, dtype=torch.uint8) if incoming else None
-        off = 0
-        for r, k in outgoing:
-            ops.append(self.dist.P2POp(self.dist.isend, src[off * node_bytes:(off + k) * node_bytes], r))
-            off += k
-        off = 0
-        for d, k in incoming:
-            ops.append(self.dist.P2POp(self.dist.irecv, dst[off * node_bytes:(off + k) * node_bytes], d))
-            off += k
-        for w in self.dist.batch_isend_irecv(ops):
-            w.wait()
-        if incoming:
-            if on_device:
-                self.sync_device()
-                engine.import_from(dst.data_ptr(), total_in)
-            else:
+            self._p2p(outgoing, incoming, src, dst, node_bytes)
+            if incoming:
                 engine.push(dst.numpy().reshape(total_in, node_bytes))
         self.bytes_sent += total_out * node_bytes
         self.bytes_recv += total_in * node_bytes
         return total_out, total_in
 
+    def _p2p(self, outgoing, incoming, src, dst, node_bytes: int) -> None:
+        """Grouped isend/irecv; with RCCL, wait() only orders the current (transfer)
+        stream after the communication — the host does not block."""
+        dist = self.dist
+        ops = []
+        off = 0
+        for r, k in outgoing:
+            ops.append(dist.P2POp(dist.isend, src[off * node_bytes:(off + k) * node_bytes], r))
+            off += k
+        off = 0
+        for d, k in incoming:
+            ops.append(dist.P2POp(dist.irecv, dst[off * node_bytes:(off + k) * node_bytes], d))
+            off += k
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
 
-def plan_sharing(sizes, m: int, cap: int, node_of=None, intra: bool = True, inter: bool = True):
-    """Deterministic steal-half matching computed identically on every rank.
+
+def plan_sharing(sizes, m: int, cap: int, node_of=None, intra: bool = True, inter: bool = True,
+                 donor_min: int | None = None):
+    """Deterministic steal-half matching computed identically on every rank
+    (Python reference of the native plan_transfers in csrc/core/dist_rounds.hpp,
+    which the runtime uses; tests check that the two agree).
 
     needy  = ranks whose pool holds fewer than m nodes (ref popBackBulk threshold),
-    donors = ranks with at least 2m nodes (ref steal condition `size >= 2*m`).
+    donors = ranks with at least donor_min (default 2m) nodes (ref `size >= 2*m`).
     Each needy rank is served by the donor with the most nodes left, which hands
     over half of what it has (capped at `cap`, ref 5*M). intra/inter restrict pairs
     to the same node (-w) or to different nodes (-L)."""
@@ -276,8 +333,9 @@ def plan_sharing(sizes, m: int, cap: int, node_of=None, intra: bool = True, inte
     needy = [r for r in range(n) if sizes[r] < m]
     needy_set = set(needy)
     plan = []
+    dmin = 2 * m if donor_min is None else donor_min
     for r in needy:
-        cands = [d for d in range(n) if left[d] >= 2 * m and d not in needy_set and
+        cands = [d for d in range(n) if left[d] >= dmin and d not in needy_set and
                  ((intra and node_of(d) == node_of(r)) or (inter and node_of(d) != node_of(r)))]
         if not cands:
             continue

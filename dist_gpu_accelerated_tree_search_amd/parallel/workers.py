@@ -36,10 +36,13 @@ def solve_rank(spec: dict) -> dict:
         res = None
         for _ in range(int(spec.get("repeat", 1))):
             comm.barrier()
-            res = distributed_solve(model, engine, comm, ub=spec.get("ub", 1), cfg=cfg)
+            res = distributed_solve(model, engine, comm, ub=spec.get("ub", 1), cfg=cfg,
+                                    window=opts.max_parents if backend == "gpu" else None)
         out = {"rank": comm.rank, "world": comm.world, "best": res.best, "tree": res.tree, "sol": res.sol,
                "elapsed": res.elapsed, "t_init": res.t_init, "t_search": res.t_search, "extra": res.extra,
-               "workers": [asdict(w) for w in res.workers]}
+               "workers": [asdict(w) for w in res.workers],
+               "comm": {"device_transfers": comm.device_transfers, "host_transfers": comm.host_transfers,
+                        "bytes_sent": comm.bytes_sent, "bytes_recv": comm.bytes_recv}}
         del engine
         return out
     finally:

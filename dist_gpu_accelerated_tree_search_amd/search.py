@@ -130,19 +130,36 @@ def solve_workers(model, devices=(0,), cpu_threads: int = 0, ub: int = 1, m: int
     from .parallel.runtime import round_robin_share
 
     init = [np.ascontiguousarray(nodes[round_robin_share(len(nodes), w, W)]) for w in range(W)]
+    # per-worker sharing thresholds: a GPU is needy below a quarter of its parent
+    # window and donates from one window; a CPU worker keeps the reference's m / 2m
+    # and receives at most 4*T nodes per steal (ref pfsp_multigpu_cuda.c:369-372)
+    o = opts or EngineOptions()
+    needy, donor, rcap = [], [], []
+    for e in engines:
+        if e.device >= 0:
+            nb = max(m, int(o.max_parents) // 4)
+            needy.append(nb)
+            donor.append(max(2 * nb, int(o.max_parents)))
+            rcap.append(steal_cap)
+        else:
+            needy.append(m)
+            donor.append(2 * m)
+            rcap.append(min(steal_cap, 4 * int(o.cpu_batch)))
     t1 = time.perf_counter()
     out = mod.run_workers(engines, init, int(best), m=m, steal_cap=steal_cap, slice_min=slice_min,
                           slice_max=slice_max, ws=ws, pin=pin, device_steals=device_steals,
-                          watchdog_s=watchdog_s, faults=dict(faults or {}))
+                          watchdog_s=watchdog_s, faults=dict(faults or {}), needy_below=needy, donor_min=donor,
+                          recv_cap=rcap)
     t2 = time.perf_counter()
     ws_ = out["workers"]
     tree = tree1 + sum(int(w["tree"]) for w in ws_)
     sol = sol1 + sum(int(w["sol"]) for w in ws_)
     workers = [WorkerStats(tree=int(w["tree"]), sol=int(w["sol"]), gen_child=int(w["tree"]),
-                           steals=int(w["transfers_in"]), success_steals=int(w["transfers_in"]),
-                           terminations=int(w["rounds"]), t_memcpy=float(w["t_memcpy"]),
+                           steals=int(w["steals"]), success_steals=int(w["success_steals"]),
+                           terminations=int(w["idle_rounds"]), t_memcpy=float(w["t_memcpy"]),
                            t_malloc=float(w["t_malloc"]), t_kernel=float(w["t_run_w"]),
-                           t_pool_ops=float(w["t_comm"]), t_idle=float(w["t_idle"])) for w in ws_]
+                           t_pool_ops=float(w["t_comm"]), t_idle=float(w["t_idle"]),
+                           t_termination=float(w["t_termination"])) for w in ws_]
     return SolveResult(best=min(int(best), int(out["best"])), tree=tree, sol=sol, elapsed=t2 - t0,
                        t_init=t1 - t0, t_search=t2 - t1, workers=workers,
                        extra={"rounds": max(int(w["rounds"]) for w in ws_), "engines": engines,

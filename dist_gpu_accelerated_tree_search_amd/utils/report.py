@@ -87,6 +87,9 @@ class WorkerStats:
     t_pool_ops: float = 0.0
     t_idle: float = 0.0
     t_termination: float = 0.0
+    # distributed runs: transfers received (DWS, ref nbSDistLoadBal) and time spent moving nodes (timeLoadBal)
+    dist_load_bal: int = 0
+    t_load_bal: float = 0.0
 
     @classmethod
     def from_dict(cls, d: dict) -> "WorkerStats":

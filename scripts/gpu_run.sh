@@ -1,0 +1,32 @@
+#!/bin/bash
+# Parameterised GPU-box session: scripts/gpu_run.sh <out-dir> <step>...
+# steps: tests[:<pytest -k expr>] | bench1 | bench2shared | smoke | prof:<name>:<cmd...>
+# Every step runs under its own timeout; the session stops at the first failure.
+set -o pipefail
+out=gpurun_out/$1; shift
+mkdir -p "$out"
+for step in "$@"; do
+  case "$step" in
+    tests*)
+      k="${step#tests}"; k="${k#:}"
+      echo "[gpu_run] pytest -m gpu ${k:+-k $k}"
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${k:+-k "$k"} \
+        > "$out/gpu_tests.log" 2>&1 || { tail -30 "$out/gpu_tests.log"; exit 1; }
+      tail -3 "$out/gpu_tests.log" ;;
+    bench1)
+      timeout -k 10 180 python bench.py --steps 20 --warmup 5 > "$out/bench_n1.json" 2> "$out/bench_n1.err" \
+        || { tail -20 "$out/bench_n1.err"; exit 1; }
+      cat "$out/bench_n1.json" ;;
+    bench2shared)
+      timeout -k 10 180 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --comm gloo --device 0 \
+        > "$out/bench_n2_shared.json" 2> "$out/bench_n2_shared.err" || { tail -20 "$out/bench_n2_shared.err"; exit 1; }
+      cat "$out/bench_n2_shared.json"; grep "last step" "$out/bench_n2_shared.err" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
+        || { tail -20 "$out/smoke.log"; exit 1; }
+      tail -1 "$out/smoke.log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[gpu_run] all steps ok"

@@ -43,6 +43,41 @@ def test_plan_sharing_properties():
     assert all(d == 1 for d, _, _ in p)
 
 
+def test_native_plan_matches_python_reference():
+    import random
+
+    from dist_gpu_accelerated_tree_search_amd import ops
+
+    C = ops.cpu()
+    rng = random.Random(7)
+    for _ in range(400):
+        n = rng.randint(1, 9)
+        sizes = [rng.choice([0, 0, 3, 30, 100, 5000, rng.randint(0, 10**6)]) for _ in range(n)]
+        m = rng.choice([1, 25, 100])
+        dmin = rng.choice([None, 2 * m, 10 * m])
+        cap = rng.choice([50, 10**4, 10**7])
+        lw = rng.choice([0, 1, 2, n])
+        intra, inter = rng.choice([(True, True), (True, False), (False, True)])
+        node_of = (lambda r, lw=lw: r // lw) if lw else None
+        ref = plan_sharing(sizes, m, cap, node_of, intra, inter, donor_min=dmin)
+        got = C.plan_transfers(sizes, m, 2 * m if dmin is None else dmin, cap, lw, intra, inter)
+        assert [tuple(t) for t in got] == ref, (sizes, m, dmin, cap, lw, intra, inter)
+
+
+def test_skewed_start_is_balanced():
+    # every Step-1 node starts on rank 0; steal-half rounds must spread the tree
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu",
+            "dist": {"start_on": 0, "split": False, "init_per_rank": 25}}
+    res = spawn_local(4, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == GOLD
+    per = [w["tree"] for w in res[0]["workers"]]
+    mean = sum(per) / len(per)
+    assert max(per) <= 1.5 * mean, per
+    assert sum(res[0]["extra"]["received_nodes"]) > 0
+    assert all(w["success_steals"] >= 1 for w in res[0]["workers"][1:])
+
+
 @pytest.mark.parametrize("world,ws,lb,ew", [(2, True, 0, True), (3, True, 1, True), (4, True, 0, True),
                                            (3, False, 0, True), (3, True, 0, False), (2, False, 1, False)])
 def test_pfsp_golden_tree(world, ws, lb, ew):
@@ -120,6 +155,49 @@ def test_checkpoint_and_resume_on_a_different_world(tmp_path):
     res = spawn_local(3, solve_rank, (spec,), timeout=300)
     assert res[0]["extra"]["complete"] is True
     assert (res[0]["tree"], res[0]["sol"], res[0]["best"]) == GOLD
+
+
+def test_checkpoint_chain_with_periodic_snapshots(tmp_path):
+    # stop at world 2, resume at world 3 with periodic checkpoints and stop again,
+    # then finish at world 2: rounds are counted over the whole solve, and a resume
+    # never sees checkpoints of two world sizes
+    import glob
+    import os
+
+    d = str(tmp_path / "ck")
+    base = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu"}
+    tiny = {"slice_min_s": 0.0002, "slice_max_s": 0.0004}
+    r1 = spawn_local(2, solve_rank, ({**base, "dist": {"max_rounds": 3, "checkpoint_dir": d, **tiny}},), timeout=300)
+    assert r1[0]["extra"]["complete"] is False and r1[0]["extra"]["rounds"] == 3
+    r2 = spawn_local(3, solve_rank, ({**base, "dist": {"resume": True, "checkpoint_dir": d, "checkpoint_every": 2,
+                                                       "max_rounds": 8, **tiny}},), timeout=300)
+    assert r2[0]["extra"]["rounds"] == 8
+    worlds = {os.path.basename(f).split("_of")[1] for f in glob.glob(os.path.join(d, "ckpt_rank*_of*.npz"))}
+    assert len(worlds) == 1
+    if r2[0]["extra"]["complete"]:
+        assert (r2[0]["tree"], r2[0]["sol"], r2[0]["best"]) == GOLD
+        return
+    r3 = spawn_local(2, solve_rank, ({**base, "dist": {"resume": True, "checkpoint_dir": d}},), timeout=300)
+    assert r3[0]["extra"]["complete"] is True
+    assert (r3[0]["tree"], r3[0]["sol"], r3[0]["best"]) == GOLD
+
+
+def test_checkpoint_while_still_replicated(tmp_path):
+    # max_rounds stops the solve before the in-search split: rank 0 saves the one
+    # (replicated) pool as a world-1 checkpoint, and the resume completes the tree
+    d = str(tmp_path / "rep")
+    base = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu"}
+    r1 = spawn_local(2, solve_rank, ({**base, "dist": {"max_rounds": 1, "checkpoint_dir": d, "split_per_rank": 10**7,
+                                                       "slice_min_s": 0.0001, "slice_max_s": 0.0001}},),
+                     timeout=300)
+    assert r1[0]["extra"]["complete"] is False
+    from dist_gpu_accelerated_tree_search_amd.parallel import checkpoint
+
+    import os
+    assert os.path.exists(os.path.join(d, "ckpt_rank0_of1.npz"))
+    r2 = spawn_local(2, solve_rank, ({**base, "dist": {"resume": True, "checkpoint_dir": d}},), timeout=300)
+    assert (r2[0]["tree"], r2[0]["sol"], r2[0]["best"]) == GOLD
+    assert checkpoint is not None
 
 
 def test_checkpoint_rejects_another_model(tmp_path):

@@ -1,5 +1,8 @@
 """Distributed runtime with GPU engines on one MI355X (ranks share the device; the
-status/steal protocol runs over gloo, nodes leave and enter the device pools)."""
+status/steal protocol runs over gloo). Nodes leave and enter the device pools
+through the device-staged branch of Comm.execute_transfers (engine.export_to into
+a device buffer on the transfer stream, a host hop around the gloo send/recv,
+engine.import_from), so only the RCCL call itself is not exercised here."""
 import pytest
 
 from dist_gpu_accelerated_tree_search_amd.parallel.launch import spawn_local
@@ -23,3 +26,21 @@ def test_gpu_ranks_queens():
             "engine": {"ring_bytes": 1 << 28, "max_parents": 1 << 12}, "dist": {"slice_min_s": 0.0001}}
     res = spawn_local(2, solve_rank, (spec,), timeout=600)
     assert (res[0]["tree"], res[0]["sol"]) == (4674889, 73712)
+
+
+def test_gpu_skewed_start_is_balanced_through_device_staging():
+    # every Step-1 node starts on rank 0; GPU-scale thresholds (window 2^14: needy
+    # below 4096 nodes, donors from 16384) must spread ta008 LB1_d over 4 ranks
+    spec = {"problem": "pfsp", "inst": 8, "lb": 0, "backend": "gpu", "comm": "gloo", "device": 0,
+            "engine": {"ring_bytes": 1 << 28, "max_parents": 1 << 14},
+            "dist": {"start_on": 0, "split": False, "init_per_rank": 25}}
+    res = spawn_local(4, solve_rank, (spec,), timeout=600)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == (113458723, 808498, 1206)
+    per = [w["tree"] for w in res[0]["workers"]]
+    mean = sum(per) / len(per)
+    assert max(per) <= 1.5 * mean, per
+    assert res[0]["extra"]["needy_below"] == 4096 and res[0]["extra"]["donor_min"] == 16384
+    assert sum(r["comm"]["device_transfers"] for r in res) > 0
+    assert sum(r["comm"]["host_transfers"] for r in res) == 0
+    assert sum(res[0]["extra"]["sent_nodes"]) == sum(res[0]["extra"]["received_nodes"]) > 0

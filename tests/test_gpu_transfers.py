@@ -1,0 +1,63 @@
+"""Device pool transfers: stream-ordered export/import between engines and the
+pinned, asynchronous spill/refill of the ring bottom (csrc/hip/engine.hpp,
+csrc/hip/host_spill.hpp)."""
+import numpy as np
+import pytest
+
+from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel
+from dist_gpu_accelerated_tree_search_amd.search import solve_engine
+
+pytestmark = pytest.mark.gpu
+GOLD14 = (2573652, 2648, 1377)
+
+
+@pytest.mark.parametrize("ub", [1, 0])
+def test_pinned_spill_and_refill_keep_the_tree(ub):
+    # a ring far too small for the pool: the bottom goes to pinned host blocks and
+    # comes back; with -u 1 the tree is deterministic, so no node may be lost
+    model = PfspModel(14, 1)
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1024, ring_bytes=1 << 20))
+    r = solve_engine(model, eng, ub=ub)
+    st = eng.stats()
+    assert r.best == 1377
+    if ub == 1:
+        assert (r.tree, r.sol) == GOLD14[:2]
+    assert st["spilled"] > 0 and st["refilled"] > 0 and st["pinned_bytes"] > 0, st
+    assert st["host_nodes"] == 0 and st["device_nodes"] == 0
+
+
+def test_export_import_between_engines_keeps_the_tree():
+    import torch
+
+    model = PfspModel(14, 1)
+    opts = EngineOptions(max_parents=1 << 12, ring_bytes=1 << 28)
+    a, b = model.make_engine("gpu", 0, opts), model.make_engine("gpu", 0, opts)
+    nodes, t1, s1, best = model.warmup(model.initial_best(1), 200)
+    a.begin(nodes, int(best))
+    b.begin(nodes[:0], int(best))
+    a.run(max_launches=2)
+    n = a.size() // 2
+    buf = torch.empty(n * model.node_bytes, dtype=torch.uint8, device="cuda:0")
+    assert a.transfer_stream != 0
+    got = a.export_to(buf.data_ptr(), n)
+    assert got == n
+    a.fence()  # host-side handoff between two engines of one process
+    b.import_from(buf.data_ptr(), n)
+    assert b.size() == n
+    a.run()
+    b.run()
+    sa, sb = a.stats(), b.stats()
+    assert (t1 + sa["tree"] + sb["tree"], s1 + sa["sol"] + sb["sol"]) == GOLD14[:2]
+    assert sa["exports"] == 1 and sb["imports"] == 1
+
+
+def test_pop_push_roundtrip_preserves_nodes():
+    model = PfspModel(14, 1)
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1024, ring_bytes=1 << 20))
+    nodes, _, _, best = model.warmup(model.initial_best(1), 100000)
+    eng.begin(nodes, int(best))  # more than half the ring: the rest goes to the pinned spill
+    st = eng.stats()
+    assert st["host_nodes"] > 0
+    out = eng.pop(len(nodes))
+    assert len(out) == len(nodes)
+    assert sorted(map(bytes, np.asarray(out))) == sorted(map(bytes, np.asarray(nodes)))
