@@ -115,7 +115,9 @@ inline void bind_engine(py::module_& m) {
       .def_property_readonly("transfer_stream", &IEngine::transfer_stream,
                              "Stream on which work-sharing sends/receives are enqueued (0: host engine).")
       .def("fence", &IEngine::fence, py::call_guard<py::gil_scoped_release>(),
-           "Wait on the host for every copy enqueued so far.");
+           "Wait on the host for every copy enqueued so far.")
+      .def("pool_weight", &IEngine::pool_weight, py::arg("w"), py::call_guard<py::gil_scoped_release>(),
+           "Sum over the pool of w[depth] (progress measure, see search.progress_weights).");
 }
 
 // Intra-node control plane (csrc/core/shm_control.hpp), bound in both modules so the
@@ -233,29 +235,29 @@ inline void bind_dist_rounds(py::module_& m) {
           py::gil_scoped_release nogil;
           out = run_dist_rounds(e, *ctl, opt, xfer, hook, rounds0);
         }
+        // per-rank table as two arrays (one row per rank): cheap to hand to Python
+        const py::ssize_t W = static_cast<py::ssize_t>(out.tree.size());
+        py::array_t<int64_t> iv({W, static_cast<py::ssize_t>(11)});
+        py::array_t<double> fv({W, static_cast<py::ssize_t>(7)});
+        auto I = iv.mutable_unchecked<2>();
+        auto F = fv.mutable_unchecked<2>();
+        for (py::ssize_t r = 0; r < W; ++r) {
+          const unsigned long long cols[11] = {out.tree[r], out.sol[r], out.sent[r], out.received[r],
+                                               out.transfers_in[r], out.transfers_out[r], out.steals[r],
+                                               out.success_steals[r], out.idle_rounds[r], out.early_rounds[r],
+                                               out.dropped[r]};
+          for (int k = 0; k < 11; ++k) I(r, k) = static_cast<int64_t>(cols[k]);
+          const double dc[7] = {out.t_run[r], out.t_comm[r], out.t_idle[r], out.t_termination[r], out.t_load_bal[r],
+                                out.t_memcpy[r], out.t_malloc[r]};
+          for (int k = 0; k < 7; ++k) F(r, k) = dc[k];
+        }
         py::dict d;
         d["best"] = out.best;
         d["complete"] = out.complete;
         d["rounds"] = out.rounds;
         d["watchdog_events"] = out.watchdog_events;
-        d["tree"] = out.tree;
-        d["sol"] = out.sol;
-        d["sent"] = out.sent;
-        d["received"] = out.received;
-        d["transfers_in"] = out.transfers_in;
-        d["transfers_out"] = out.transfers_out;
-        d["steals"] = out.steals;
-        d["success_steals"] = out.success_steals;
-        d["idle_rounds"] = out.idle_rounds;
-        d["early_rounds"] = out.early_rounds;
-        d["dropped"] = out.dropped;
-        d["t_run"] = out.t_run;
-        d["t_comm"] = out.t_comm;
-        d["t_idle"] = out.t_idle;
-        d["t_termination"] = out.t_termination;
-        d["t_load_bal"] = out.t_load_bal;
-        d["t_memcpy"] = out.t_memcpy;
-        d["t_malloc"] = out.t_malloc;
+        d["counts"] = iv;  // tree sol sent received transfers_in transfers_out steals success_steals idle_rounds early_rounds dropped
+        d["times"] = fv;   // t_run t_comm t_idle t_termination t_load_bal t_memcpy t_malloc
         return d;
       },
       py::arg("engine"), py::arg("shm_address"), py::arg("allgather_fn"), py::arg("rank"), py::arg("world"),

@@ -7,6 +7,7 @@
 
 #include "../core/cpu_engine.hpp"
 #include "../core/drivers_cpu.hpp"
+#include "../core/estimate.hpp"
 #include "../core/shm_control.hpp"
 #include "engine_binding.hpp"
 
@@ -166,6 +167,36 @@ PYBIND11_MODULE(_tts_cpu, m) {
         });
       },
       py::arg("inst"), py::arg("lb"), py::arg("best"), py::arg("target"));
+  m.def(
+      "tree_estimate",
+      [](py::object problem, int best, unsigned long long probes, unsigned long long seed, int threads) {
+        auto pack = [](const TreeEstimate& e) {
+          py::dict d;
+          d["tree"] = e.tree;
+          d["stderr"] = e.stderr_;
+          d["depth"] = e.depth;
+          d["probes"] = e.probes;
+          d["per_level"] = e.per_level;
+          return d;
+        };
+        TreeEstimate e;
+        if (py::hasattr(problem, "native") && py::isinstance<PfspInstance>(problem.attr("native"))) {
+          const PfspInstance& in = problem.attr("native").cast<const PfspInstance&>();
+          const int lb = problem.attr("host_lb").cast<int>();
+          py::gil_scoped_release nogil;
+          e = with_pfsp_bucket(in.jobs, [&](auto nj) {
+            constexpr int NJ = decltype(nj)::value;
+            return knuth_estimate(PfspProblem<NJ>(in, lb), best, probes, seed, threads);
+          });
+        } else {
+          QueensProblem q(problem.attr("N").cast<int>(), problem.attr("G").cast<int>());
+          py::gil_scoped_release nogil;
+          e = knuth_estimate(q, best, probes, seed, threads);
+        }
+        return pack(e);
+      },
+      py::arg("model"), py::arg("best"), py::arg("probes") = 1000, py::arg("seed") = 1, py::arg("threads") = 1,
+      "Knuth random-probe estimate of the explored tree for a fixed incumbent (core/estimate.hpp).");
   m.def(
       "pfsp_drain",
       [](const PfspInstance& in, int lb, int best, U8 nodes) {

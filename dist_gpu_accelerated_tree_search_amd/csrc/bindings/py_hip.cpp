@@ -136,6 +136,27 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("device") = 0);
 
   m.def(
+      "pfsp_expand_probe",
+      [](int jobs, int machines, std::vector<int> p, int lb, U8 parents, int best, int device, int variant) {
+        const PfspInstance in = make_instance(jobs, machines, std::move(p));
+        const size_t nb = with_pfsp_bucket(jobs, [](auto nj) { return sizeof(PfspNode<decltype(nj)::value>); });
+        if (parents.ndim() != 2 || static_cast<size_t>(parents.shape(1)) != nb)
+          throw std::invalid_argument("parents must be a (n, node_bytes) uint8 array");
+        std::vector<int> out;
+        {
+          py::gil_scoped_release nogil;
+          out = pfsp_expand_probe(in, lb, parents.data(), static_cast<size_t>(parents.shape(0)), best, device, variant);
+        }
+        py::array_t<int> r(static_cast<py::ssize_t>(out.size()));
+        std::memcpy(r.mutable_data(), out.data(), out.size() * sizeof(int));
+        return r;
+      },
+      py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("parents"), py::arg("best") = INT_MAX,
+      py::arg("device") = 0, py::arg("variant") = 0,
+      "One production expand iteration over these parents with the debug output on: every child's bound "
+      "(exact LB2 below best, else >= best). variant 0 prefix/suffix, 1 rounds, 2 dense, 3 wave.");
+
+  m.def(
       "queens_labels",
       [](int N, int G, U8 parents, int device) {
         if (parents.ndim() != 2 || parents.shape(1) != static_cast<py::ssize_t>(sizeof(QueensNode)))

@@ -100,6 +100,13 @@ class CpuEngine final : public IEngine {
   }
   bool split_pending() override { return split_world_ > 1 && !split_done_; }
   void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
+  double pool_weight(const std::vector<double>& w) override {
+    double s = 0;
+    if (w.empty()) return s;
+    for (size_t i = 0; i < pool_.size(); ++i)
+      s += w[std::min<size_t>(static_cast<size_t>(pool_.data()[i].depth), w.size() - 1)];
+    return s;
+  }
   EngineStats solve_from(const void* nodes, size_t n, int best) override {
     begin(nodes, n, best);
     run(-1, 0.0, 0);
@@ -224,6 +231,7 @@ class OwningCpuEngine final : public IEngine {
   void set_split(int r, int w, size_t mp) override { eng_.set_split(r, w, mp); }
   bool split_pending() override { return eng_.split_pending(); }
   void set_progress_hook(ProgressHook h) override { eng_.set_progress_hook(std::move(h)); }
+  double pool_weight(const std::vector<double>& w) override { return eng_.pool_weight(w); }
   void set_best(int b) override { eng_.set_best(b); }
   int best() override { return eng_.best(); }
   void reset_counters() override { eng_.reset_counters(); }

@@ -6,6 +6,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <vector>
 
 namespace tts {
 
@@ -59,6 +60,10 @@ class IEngine {
   virtual uintptr_t transfer_stream() const { return 0; }
   virtual void fence() {}
   virtual void set_progress_hook(ProgressHook hook) { (void)hook; }
+  // Sum over the pool of w[depth] (clamped to the last entry): with w[d] the share
+  // of the search space below a node of depth d, 1 - pool_weight is the explored
+  // fraction of the space (the B&B progress measure of tools/progress estimates).
+  virtual double pool_weight(const std::vector<double>& w) { (void)w; return 0; }
   virtual size_t size() = 0;
   // Replays expand graphs until the pool is empty, `max_launches` graphs were
   // launched (<0: unlimited), `max_seconds` elapsed (<=0: unlimited), or the pool

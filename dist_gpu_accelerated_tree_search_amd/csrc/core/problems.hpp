@@ -92,12 +92,23 @@ struct QueensProblem {
       return;
     }
     uint32_t safe = ~(parent.cols | parent.diag | parent.anti) & full();
-    // -g: the safety predicate is evaluated G times (artificial work multiplier,
-    // ref nqueens_c.c:80-96); the barrier keeps the repeats from being folded.
-    for (int g = 1; g < G; ++g) {
-      uint32_t again = ~(parent.cols | parent.diag | parent.anti) & full();
-      asm volatile("" : "+r"(again));
-      safe &= again;
+    // -g > 1: the reference's artificial work (ref nqueens_c.c:80-96): each candidate
+    // row is tested G times against the `depth` placed queens — G * depth dependent
+    // compares per candidate, kept by the barrier (see queens_free_rows on the GPU).
+    if (G > 1) {
+      const uint32_t att = parent.diag | parent.anti;
+      uint32_t cand = ~parent.cols & full();
+      while (cand) {
+        const uint32_t bit = cand & (0u - cand);
+        cand ^= bit;
+        uint32_t hit = 0;
+        for (int g = 0; g < G; ++g)
+          for (uint32_t i = 0; i < parent.depth; ++i) {
+            hit |= att & bit;
+            asm volatile("" : "+r"(hit));
+          }
+        safe &= ~hit;
+      }
     }
     while (safe) {
       const uint32_t bit = safe & (0u - safe);

@@ -266,6 +266,35 @@ class DeviceEngine final : public IEngine {
     return dev_total() + spill_.size() + refill_n_;
   }
 
+  double pool_weight(const std::vector<double>& w) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    if (w.empty()) return 0;
+    settle();
+    normalize();
+    upload_ctl();
+    double* dw = nullptr;
+    TTS_HIP_CHECK(hipMalloc(&dw, (w.size() + 1) * sizeof(double)));
+    TTS_HIP_CHECK(hipMemcpyAsync(dw, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice, stream_));
+    TTS_HIP_CHECK(hipMemsetAsync(dw + w.size(), 0, sizeof(double), stream_));
+    const size_t n = dev_stack();
+    if (n) {
+      const int blocks = static_cast<int>(std::min<size_t>((n + dev::kBlock - 1) / dev::kBlock, 4096));
+      hipLaunchKernelGGL(dev::pool_weight_kernel<Node>, dim3(blocks), dim3(dev::kBlock), 0, stream_, d_ring_,
+                         static_cast<dev::u64>(cap_ - 1), static_cast<dev::u64>(h_ctl_->bot), static_cast<dev::u64>(n),
+                         dw, static_cast<int>(w.size()), dw + w.size());
+      TTS_HIP_CHECK(hipGetLastError());
+    }
+    double dev_sum = 0;
+    TTS_HIP_CHECK(hipMemcpyAsync(&dev_sum, dw + w.size(), sizeof(double), hipMemcpyDeviceToHost, stream_));
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    (void)hipFree(dw);
+    std::vector<Node> host;
+    spill_.snapshot(host);
+    double host_sum = 0;
+    for (const Node& x : host) host_sum += w[std::min<size_t>(static_cast<size_t>(x.depth), w.size() - 1)];
+    return dev_sum + host_sum;
+  }
+
   long run(long max_launches, double max_seconds, size_t stop_below) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     const auto t0 = std::chrono::steady_clock::now();
@@ -672,13 +701,16 @@ class DeviceEngine final : public IEngine {
   // pool when the copy has completed (fold_refill). Returns false without room.
   bool start_refill(size_t want) {
     if (refill_n_ || spill_.empty() || want == 0) return false;
-    const size_t used = dev_total() + reserved_ + static_cast<size_t>(ks_.back() + 1) * buf_nodes_;
-    if (used >= cap_) return false;
+    // like push_host: the device part stays within half the ring (the rest is
+    // growth room for the replays, checked by pick_graph)
+    const size_t used = dev_total() + reserved_;
+    if (used >= cap_ / 2) return false;
     const size_t b0 = h_ctl_->bot & (cap_ - 1);
-    size_t k = std::min({want, spill_.size(), cap_ - used, b0 ? b0 : cap_});
-    Node* dst = d_ring_ + ((b0 + cap_ - k) & (cap_ - 1));
-    k = spill_.pop_to_device(dst, k, xfer_, &refill_ev_);
+    // one pinned block at most, contiguous under the ring bottom
+    const size_t k = std::min({want, spill_.top_count(), cap_ / 2 - used, b0 ? b0 : cap_});
     if (k == 0) return false;
+    Node* dst = d_ring_ + ((b0 + cap_ - k) & (cap_ - 1));
+    if (spill_.pop_to_device(dst, k, xfer_, &refill_ev_) != k) throw std::logic_error("pinned spill: short refill");
     refill_n_ = k;
     reserved_ += k;
     return true;

@@ -43,6 +43,11 @@ class PinnedSpill {
   PinnedSpill& operator=(const PinnedSpill&) = delete;
 
   size_t size() const { return n_; }
+  // Nodes the next pop_to_device can return at most (the newest block's).
+  size_t top_count() {
+    trim();
+    return blocks_.empty() ? 0 : blocks_.back().hi - blocks_.back().lo;
+  }
   bool empty() const { return n_ == 0; }
   size_t block_nodes() const { return block_nodes_; }
 

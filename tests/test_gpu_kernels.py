@@ -58,9 +58,43 @@ def test_pfsp_bounds_root_and_leaf_parents():
     assert np.array_equal(model.child_bounds_gpu(deep), model.child_bounds_cpu(deep))
 
 
-@pytest.mark.parametrize("N,G", [(8, 1), (14, 1), (20, 3), (32, 1)])
+@pytest.mark.parametrize("N,G", [(8, 1), (14, 1), (20, 3), (32, 1), (32, 4)])
 def test_queens_labels_match_cpu(N, G):
     C = ops.cpu()
-    nodes, _, _ = C.queens_bfs(min(N, 12), 1, 2000)
-    model = QueensModel(min(N, 12), G)
+    nodes, _, _ = C.queens_bfs(N, 1, 2000 if N > 10 else 100)
+    assert len(nodes) > 0 and int(nd.queens_unpack(nodes)[3].max()) >= 2
+    model = QueensModel(N, G)
     assert np.array_equal(model.labels_gpu(nodes), model.labels_cpu(nodes))
+
+
+@pytest.mark.parametrize("inst,best_from", [(3, None), (14, None), (21, None), (56, None), (81, None), (101, None),
+                                            (14, "opt"), (56, "opt"), (21, "opt")])
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_lb2_expand_path_matches_cpu(inst, best_from, variant):
+    # the production LB2 expand kernel (B1 LB1 filter, learned pair order, B2 walks:
+    # prefix/suffix (0), rounds (1), dense (2); B3 decision) against cpu_lb2 child
+    # by child: exact values when best = INT_MAX, the lb < best decision otherwise
+    model = PfspModel(inst, 2)
+    n = {20: 600, 50: 200, 100: 40}.get(model.jobs, 12)
+    nodes = random_nodes(model.jobs, n, inst * 7 + variant)
+    best = INT_MAX if best_from is None else model.best_known
+    H = ops.require_gpu(0)
+    gpu = H.pfsp_expand_probe(model.jobs, model.machines, list(model.native.p), 2, nodes, best, 0, variant)
+    cpu = model.child_bounds_cpu(nodes, INT_MAX)
+    assert gpu.shape == cpu.shape
+    if best == INT_MAX:
+        assert np.array_equal(gpu, cpu), f"{(gpu != cpu).sum()} mismatches"
+    else:
+        assert np.array_equal(gpu < best, cpu < best), f"{((gpu < best) != (cpu < best)).sum()} decisions differ"
+        below = cpu < best
+        assert np.array_equal(gpu[below], cpu[below])
+
+
+@pytest.mark.parametrize("inst", [101, 111])
+def test_lb2_bounds_large_buckets(inst):
+    model = PfspModel(inst, 2)
+    nodes = random_nodes(model.jobs, 4, inst)
+    assert np.array_equal(model.child_bounds_gpu(nodes), model.child_bounds_cpu(nodes))
+    H = ops.require_gpu(0)
+    gpu = H.pfsp_expand_probe(model.jobs, model.machines, list(model.native.p), 2, nodes, INT_MAX, 0, 0)
+    assert np.array_equal(gpu, model.child_bounds_cpu(nodes))
