@@ -58,17 +58,24 @@ struct PfspTableImages {
   std::vector<uint2> pinfo;    // [P]
 };
 
+// Machine counts below the kernel's M are padded with trailing machines of zero
+// processing time: the makespan, every LB1 machine term and the fronts of the real
+// machines are unchanged (a zero machine after the last one completes with it), and
+// LB2 walks only the instance's own pairs (npairs), so the bounds equal the host
+// oracle's for the real instance.
 template <int NJ, int M>
 inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, M>& a, bool pair_order = false) {
   using C = dev::PfspConsts<M>;
-  if (in.machines != M) throw std::invalid_argument("machine count does not match kernel instantiation");
+  if (in.machines > M || in.machines < 1) throw std::invalid_argument("machine count exceeds kernel instantiation");
   if (in.jobs > NJ) throw std::invalid_argument("job count exceeds kernel bucket");
+  const int MR = in.machines;
+  const int PR = MR * (MR - 1) / 2;
   PfspTableImages img;
   img.ptab.assign(static_cast<size_t>(in.jobs) * C::MS, 0);
   for (int j = 0; j < in.jobs; ++j)
-    for (int m = 0; m < M; ++m) img.ptab[static_cast<size_t>(j) * C::MS + m] = static_cast<uint16_t>(in.pt(m, j));
-  img.recs.resize(static_cast<size_t>(C::P) * in.jobs);
-  for (int q = 0; q < C::P; ++q) {
+    for (int m = 0; m < MR; ++m) img.ptab[static_cast<size_t>(j) * C::MS + m] = static_cast<uint16_t>(in.pt(m, j));
+  img.recs.resize(static_cast<size_t>(PR) * in.jobs);
+  for (int q = 0; q < PR; ++q) {
     const int m0 = in.pair_m0[q], m1 = in.pair_m1[q];
     for (int r = 0; r < in.jobs; ++r) {
       const int job = in.johnson[static_cast<size_t>(q) * in.jobs + r];
@@ -83,12 +90,12 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
   // expand kernel's pair table in the learned early-exit order (lb2_pair_order);
   // recs stay in the reference order (the bounds kernel keeps its exact partial
   // values) and pinfo points each slot at its pair's records
-  img.pinfo.resize(C::P);
+  img.pinfo.resize(PR);
   {
-    std::vector<int> ord(C::P);
-    for (int q = 0; q < C::P; ++q) ord[q] = q;
-    if (pair_order) ord = lb2_pair_order(in);
-    for (int i = 0; i < C::P; ++i) {
+    std::vector<int> ord(PR);
+    for (int q = 0; q < PR; ++q) ord[q] = q;
+    if (pair_order && PR > 0) ord = lb2_pair_order(in);
+    for (int i = 0; i < PR; ++i) {
       const int q = ord[i];
       const int m0 = in.pair_m0[q], m1 = in.pair_m1[q];
       if (in.min_tails[m0] > 0xffff || in.min_tails[m1] > 0xffff)
@@ -98,20 +105,48 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
     }
   }
   a.jobs = in.jobs;
+  a.npairs = PR;
   for (int m = 0; m < M; ++m) {
-    a.min_heads[m] = in.min_heads[m];
-    a.min_tails[m] = in.min_tails[m];
+    if (m < MR) {
+      a.min_heads[m] = in.min_heads[m];
+      a.min_tails[m] = in.min_tails[m];
+    } else {  // padding machine: head = whole real route of the cheapest job, no tail
+      int h = INT_MAX;
+      for (int j = 0; j < in.jobs; ++j) {
+        int t = 0;
+        for (int k = 0; k < MR; ++k) t += in.pt(k, j);
+        h = std::min(h, t);
+      }
+      a.min_heads[m] = h;
+      a.min_tails[m] = 0;
+    }
     long s = 0;
-    for (int j = 0; j < in.jobs; ++j) s += in.pt(m, j);
+    if (m < MR)
+      for (int j = 0; j < in.jobs; ++j) s += in.pt(m, j);
     // front and remain are packed as two u16 per machine in LDS
     if (s > 0xffff) throw std::invalid_argument("instance too large for 16-bit schedule packing");
     a.sum_all[m] = static_cast<int>(s);
   }
-  for (int q = 0; q < C::P; ++q) {
+  for (int q = 0; q < PR; ++q) {
     a.pm0[q] = static_cast<uint8_t>(in.pair_m0[q]);
     a.pm1[q] = static_cast<uint8_t>(in.pair_m1[q]);
   }
   return img;
+}
+
+// LB2 records fit the packed 4-B LDS layout of kernel LBK 3 ({job:6 | p0:7 | p1:7 | lag:12}).
+inline bool lb2_records_pack(const PfspInstance& in) {
+  if (in.jobs > 64) return false;
+  for (int v : in.p)
+    if (v > 127) return false;
+  for (int v : in.lags)
+    if (v > 4095) return false;
+  return true;
+}
+// The 50-job LB2 kernel with every record in LDS (LBK 3): TTS_LB2_PACK=1 (A/B).
+inline bool lb2_pack_wanted(const PfspInstance& in) {
+  const char* f = std::getenv("TTS_LB2_PACK");
+  return f && std::atoi(f) != 0 && lb2_records_pack(in);
 }
 
 template <class T>
@@ -126,7 +161,7 @@ template <int NJ, int M, int LBK>
 std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const EngineConfig& cfg) {
   TTS_HIP_CHECK(hipSetDevice(cfg.device));
   dev::PfspArgs<NJ, M> a{};
-  const PfspTableImages img = pfsp_fill_args(in, a, LBK == 2);
+  const PfspTableImages img = pfsp_fill_args(in, a, LBK >= 2);
   a.ptab = upload_vec(img.ptab);
   a.recs = upload_vec(img.recs);
   a.pinfo = upload_vec(img.pinfo);
@@ -140,8 +175,12 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   a.lb2_rounds = M >= 10 ? 1 : 0;
   if (const char* f = std::getenv("TTS_LB2_ROUNDS")) a.lb2_rounds = std::atoi(f) != 0;  // A/B runs
   // prefix/suffix walks (lb2_ps_walks): O(N) per (parent, pair) instead of per
-  // (child, pair); TTS_LB2_PS=0 returns to the per-child walks above
-  a.lb2_ps = 1;
+  // (child, pair), but every live parent walks whole pair rounds. Measured slower
+  // than the per-child walks with the LB1 filter and early exit (ta056 0.081 -> 0.042
+  // G nodes/s, ta010 4.0 -> 7.4 ms, profiles/r2c: about one child per parent survives,
+  // and a survivor's full LB2 costs N steps per pair per-child vs 2N per parent):
+  // off by default, TTS_LB2_PS=1 turns it on
+  a.lb2_ps = 0;
   if (const char* f = std::getenv("TTS_LB2_PS")) a.lb2_ps = std::atoi(f) != 0;
   auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a);
   eng->adopt(const_cast<uint16_t*>(a.ptab));
@@ -265,14 +304,14 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
   }
 }
 
+// Kernel machine bucket: 5, 10 or 20 (Taillard's counts); other counts up to 20 run
+// in the next bucket with zero-time padding machines (pfsp_fill_args).
 template <class F>
 decltype(auto) with_machine_bucket(int machines, F&& f) {
-  switch (machines) {
-    case 5: return f(std::integral_constant<int, 5>{});
-    case 10: return f(std::integral_constant<int, 10>{});
-    case 20: return f(std::integral_constant<int, 20>{});
-    default: throw std::invalid_argument("GPU kernels are instantiated for 5, 10 or 20 machines");
-  }
+  if (machines >= 1 && machines <= 5) return f(std::integral_constant<int, 5>{});
+  if (machines > 5 && machines <= 10) return f(std::integral_constant<int, 10>{});
+  if (machines > 10 && machines <= 20) return f(std::integral_constant<int, 20>{});
+  throw std::invalid_argument("GPU kernels support 1 to 20 machines");
 }
 
 // ---- run-time dispatch (definitions in pfsp_engine_nj*.hip, one TU per bucket) ----
@@ -299,7 +338,10 @@ TTS_PFSP_DECLARE_BUCKET(500)
   std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg) { \
     return with_machine_bucket(in.machines, [&](auto mm) -> std::unique_ptr<IEngine> {               \
       constexpr int M = decltype(mm)::value;                                                         \
-      return lb == 2 ? make_pfsp_engine_t<NJ, M, 2>(in, cfg) : make_pfsp_engine_t<NJ, M, 1>(in, cfg); \
+      if (lb != 2) return make_pfsp_engine_t<NJ, M, 1>(in, cfg);                                    \
+      if constexpr (NJ == 50)                                                                        \
+        if (lb2_pack_wanted(in)) return make_pfsp_engine_t<NJ, M, 3>(in, cfg);                       \
+      return make_pfsp_engine_t<NJ, M, 2>(in, cfg);                                                  \
     });                                                                                              \
   }                                                                                                  \
   std::vector<int> pfsp_gpu_bounds_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \

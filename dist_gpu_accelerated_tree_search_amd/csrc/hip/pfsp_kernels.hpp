@@ -44,17 +44,17 @@ struct PfspGeom {
   // many workgroups and keep the per-chunk LDS (child fronts) small.
   static constexpr int NM = NJ * M;
   static constexpr int BP2 = NM <= 100 ? 64 :(NM <= 200 ? 16 : (NM <= 1000 ? 8 : 2));
-  static constexpr int BP = LBK == 2 ? BP2 : BP1;
+  static constexpr int BP = LBK >= 2 ? BP2 : BP1;  // LBK 3 = LB2 with packed LDS records
   // 50-job LB2 (NM 500..1000): 8-parent chunks, half as many per iteration (same
   // 16K-parent window, half the per-chunk barriers; the smaller chunk-count prefix
   // pays for the larger child arrays in LDS)
-  static constexpr int MAXCHUNKS = LBK == 2 ? (NM > 400 && NM <= 1000 ? 2048 : 4096) : 2048;
+  static constexpr int MAXCHUNKS = LBK >= 2 ? (NM > 400 && NM <= 1000 ? 2048 : 4096) : 2048;
   static constexpr int MAXCH = BP * NJ;                  // children per chunk (upper bound)
   // local DFS steps per chunk and iteration (the LB1 register path only) and the
   // chunk's slot region in the children buffers = its private stack. Two chunks'
   // worth of children: a chunk keeps stepping while one more full expansion fits,
   // and the ring's worst-case growth per iteration (engine pick_graph) only doubles.
-  static constexpr int LT = (LBK != 2 && sizeof(PfspNode<NJ>) == 32) ? 8 : 1;
+  static constexpr int LT = (LBK < 2 && sizeof(PfspNode<NJ>) == 32) ? 8 : 1;
   static constexpr int SLOT = MAXCH * (LT > 1 ? 2 : 1);
   static constexpr int NWORDS = (MAXCH + 63) / 64;       // survivor bitmap words
   static constexpr int NW = (NJ + 63) / 64;              // 64-bit words of a job set
@@ -83,6 +83,7 @@ struct PfspArgs {
   int* bounds_out;         // bounds kernel only
   const PfspNode<NJ>* parents_in;  // bounds kernel only
   int jobs;
+  int npairs;              // machine pairs of the instance (<= P: machines padded up to M, see pfsp_fill_args)
   int nparents;            // bounds kernel only
   int best_in;             // bounds kernel only
   int min_heads[M];
@@ -254,7 +255,7 @@ __device__ inline int pfsp_child_bound(const PfspArgs<NJ, M>& a, PfspSmem<NJ, M,
     const uint2* recs = SmemRecs<NJ, M, LBK>::get(a, sm);
     const int N = a.jobs;
     int lb = 0;
-    for (int q = 0; q < C::P; ++q) {
+    for (int q = 0; q < a.npairs; ++q) {
       const int ma0 = a.pm0[q], ma1 = a.pm1[q];
       int t0 = cf[ma0], t1 = cf[ma1];
       const uint2* rq = recs + q * N;
@@ -284,7 +285,7 @@ __device__ inline void pfsp_stage_tables(const PfspArgs<NJ, M>& a, PfspSmem<NJ, 
   uint16_t* pt = &sm.ptab[0][0];
   for (int i = tid; i < nrow; i += kBlock) pt[i] = a.ptab[i];
   if constexpr (PfspSmem<NJ, M, LBK>::kRecsInLds) {
-    const int nrec = C::P * a.jobs;
+    const int nrec = a.npairs * a.jobs;
     for (int i = tid; i < nrec; i += kBlock) sm.recs[i] = a.recs[i];
   }
   __syncthreads();
@@ -380,17 +381,19 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 
-template <int NJ, int M>
+template <int NJ, int M, bool PACK>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 
 // Occupancy: the LB1 kernels are latency-bound (profiles/r1o), so the register
 // budget is capped for more resident waves (6 per SIMD for M <= 10: 80 VGPRs, no
 // spills); LB2 is bounded by its LDS footprint instead.
 template <int NJ, int M, int LBK>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK == 2 ? 1 : (M <= 10 ? 6 : 4))))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
 void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
-    pfsp_expand_lb2<NJ, M>(a, t);
+    pfsp_expand_lb2<NJ, M, false>(a, t);
+  else if constexpr (LBK == 3)
+    pfsp_expand_lb2<NJ, M, true>(a, t);
   else if constexpr (sizeof(PfspNode<NJ>) == 32)
     pfsp_expand_lb1_small<NJ, M>(a, t);
   else
@@ -412,10 +415,12 @@ void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
 //       is skipped (the reference's early exit, c_bound_johnson.c:231-234: only
 //       the lb < best decision matters, and it is unchanged).
 //   B3  survivors (LB2 < best) -> ballot bitmap -> compaction as in every kernel.
-template <int NJ, int M>
+template <int NJ, int M, bool PACK = false>
 struct PfspSmemLB2 {
   using G = PfspGeom<NJ, 2, M>;
   using C = PfspConsts<M>;
+  // PACK (kernel LBK 3): every pair's records in LDS, 4 B each {job:6 | p0:7 | p1:7 |
+  // lag:12}, in evaluation order (50 x 20: 38 KB)
   // records in LDS when they fit 32 KB (20 x 20: 30 KB); otherwise (50 x 20: 76 KB)
   // they are read from L2 (packing the leading pairs to 4 B in LDS measured no gain,
   // profiles/r1ag)
@@ -442,6 +447,7 @@ struct PfspSmemLB2 {
   int red[kBlock / kWave];
   uint2 pinfo[C::P];
   uint2 recs[kRecsInLds ? C::P * NJ : 1];
+  uint32_t rpk[PACK ? C::P * NJ : 1];
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -460,7 +466,7 @@ using kconst_u64 = const __attribute__((address_space(4))) unsigned long long;  
 template <int NJ, int M, class S>
 __device__ inline void lb2_walks_wave(const PfspArgs<NJ, M>& a, S& sm, int nact, int best) {
   using G = PfspGeom<NJ, 2, M>;
-  constexpr int P = PfspConsts<M>::P;
+  const int P = a.npairs;
   constexpr int NWAVE = kBlock / kWave;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
@@ -515,7 +521,7 @@ __device__ inline void lb2_walks_wave(const PfspArgs<NJ, M>& a, S& sm, int nact,
 template <int NJ, int M, class S>
 __device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid, int nact, int best) {
   using G = PfspGeom<NJ, 2, M>;
-  constexpr int P = PfspConsts<M>::P;
+  const int P = a.npairs;
   static_assert(G::BP <= kWave, "parent list is built by one wave");
   const int tid = threadIdx.x;
   const int N = a.jobs;
@@ -593,15 +599,47 @@ __device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid,
   }
 }
 
-template <int NJ, int M>
+// One Johnson walk (ref c_bound_johnson.c:190-209) of machine pair slot `qs` (pair
+// info `pi`) from child fronts (t0, t1) over the jobs not in `msk`. Records come from
+// LDS (packed 4 B, PACK) or from `recs` (LDS or L2).
+template <int NJ, int M, bool PACK, class S>
+__device__ inline void lb2_johnson_walk(const S& sm, const uint2* recs, int qs, uint2 pi, int N,
+                                        const u64 (&msk)[PfspGeom<NJ, 2, M>::NW], int& t0, int& t1) {
+  using G = PfspGeom<NJ, 2, M>;
+  if constexpr (PACK) {
+    const uint32_t* rq = sm.rpk + qs * N;
+#pragma unroll 4
+    for (int r = 0; r < N; ++r) {
+      const uint32_t w = rq[r];
+      const int n0 = t0 + static_cast<int>((w >> 6) & 127u);
+      const int n1 = max(t1, n0 + static_cast<int>(w >> 20)) + static_cast<int>((w >> 13) & 127u);
+      const bool sched = job_in<G::NW>(msk, static_cast<int>(w & 63u));
+      t0 = sched ? t0 : n0;
+      t1 = sched ? t1 : n1;
+    }
+  } else {
+    const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
+#pragma unroll 4
+    for (int r = 0; r < N; ++r) {
+      const uint2 rc = rq[r];
+      const int n0 = t0 + static_cast<int>(rc.x >> 16);
+      const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
+      const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
+      t0 = sched ? t0 : n0;
+      t1 = sched ? t1 : n1;
+    }
+  }
+}
+
+template <int NJ, int M, bool PACK>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   using G = PfspGeom<NJ, 2, M>;
   using C = PfspConsts<M>;
-  using S = PfspSmemLB2<NJ, M>;
+  using S = PfspSmemLB2<NJ, M, PACK>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
   constexpr int NWD = sizeof(Node) / 4;
-  constexpr int P = C::P;
+  const int P = a.npairs;
   __shared__ S sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
@@ -618,6 +656,12 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     for (int i = tid; i < P; i += kBlock) sm.pinfo[i] = a.pinfo[i];
     if constexpr (S::kRecsInLds)
       for (int i = tid; i < P * a.jobs; i += kBlock) sm.recs[i] = a.recs[i];
+    if constexpr (PACK)
+      for (int i = tid; i < P * a.jobs; i += kBlock) {
+        const int slot = i / a.jobs, r = i - slot * a.jobs;
+        const uint2 rc = a.recs[static_cast<int>(a.pinfo[slot].x >> 16) * a.jobs + r];
+        sm.rpk[i] = (rc.x & 0xffffu) | ((rc.x >> 16) << 6) | ((rc.y & 0xffffu) << 13) | ((rc.y >> 16) << 20);
+      }
   }
   const uint2* recs = S::kRecsInLds ? sm.recs : a.recs;
   const int N = a.jobs;
@@ -708,16 +752,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
             u64 msk[G::NW];
 #pragma unroll
             for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
-            const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
-#pragma unroll 4
-            for (int r = 0; r < N; ++r) {
-              const uint2 rc = rq[r];
-              const int n0 = t0 + static_cast<int>(rc.x >> 16);
-              const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
-              const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
-              t0 = sched ? t0 : n0;
-              t1 = sched ? t1 : n1;
-            }
+            lb2_johnson_walk<NJ, M, PACK>(sm, recs, q0 + qq, pi, N, msk, t0, t1);
             atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
           }
           ii += di;
@@ -760,18 +795,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
           u64 msk[G::NW];
 #pragma unroll
           for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
-          {
-            const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
-#pragma unroll 4
-            for (int r = 0; r < N; ++r) {
-              const uint2 rc = rq[r];
-              const int n0 = t0 + static_cast<int>(rc.x >> 16);
-              const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
-              const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
-              t0 = sched ? t0 : n0;
-              t1 = sched ? t1 : n1;
-            }
-          }
+          lb2_johnson_walk<NJ, M, PACK>(sm, recs, q, pi, N, msk, t0, t1);
           atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
         }
         ai += da;

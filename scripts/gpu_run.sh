@@ -22,11 +22,13 @@ for step in "$@"; do
         --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --comm gloo --device 0 \
         > "$out/bench_n2_shared.json" 2> "$out/bench_n2_shared.err" || { tail -20 "$out/bench_n2_shared.err"; exit 1; }
       cat "$out/bench_n2_shared.json"; grep "last step" "$out/bench_n2_shared.err" ;;
-    lb2:*)
-      secs="${step#lb2:}"
-      timeout -k 10 $((secs + 240)) python -u scripts/lb2_probe.py "$secs" 20 > "$out/lb2_probe.txt" 2>&1 \
-        || { tail -20 "$out/lb2_probe.txt"; exit 1; }
-      cat "$out/lb2_probe.txt" ;;
+    lb2:*)  # lb2:<seconds>[@ENV=V,...]
+      arg="${step#lb2:}"; secs="${arg%%@*}"; envs=""; [ "$arg" != "$secs" ] && envs="${arg#*@}"
+      tag="lb2_probe${envs:+_$(echo "$envs" | tr ',=' '__')}"
+      ( IFS=','; for e in $envs; do export "$e"; done
+        timeout -k 10 $((secs + 240)) python -u scripts/lb2_probe.py "$secs" 10 > "$out/$tag.txt" 2>&1 ) \
+        || { tail -20 "$out/$tag.txt"; exit 1; }
+      cat "$out/$tag.txt" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
         || { tail -20 "$out/smoke.log"; exit 1; }

@@ -3,10 +3,10 @@ ta056 (50x20) run with a progress projection.
 
     python scripts/lb2_probe.py [ta056_seconds] [report_every_s]
 
-Progress: p = 1 - pool_weight, the explored share of the permutation space (a node
-of depth d stands for 1/(N(N-1)...(N-d+1)) of it; pruned subtrees count as explored).
-The projection t * (1 - p) / p assumes the remaining space is explored at the
-average rate so far; it is a rough indicator, not a bound.
+Progress: W = pool_weight, the share of the permutation space still held by the pool
+(a node of depth d stands for 1/(N(N-1)...(N-d+1)) of it; pruned subtrees count as
+explored). The projection W / (-dW/dt) uses the rate at which W fell over the last
+report interval; it is a rough indicator (B&B progress is not linear), not a bound.
 """
 import sys
 import time
@@ -39,14 +39,17 @@ nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
 eng.begin(nodes, int(best))
 t0 = time.perf_counter()
 done = False
+W0, tw = eng.pool_weight(w), 0.0
 while time.perf_counter() - t0 < secs:
     eng.run(max_seconds=every)
     st = eng.stats()
     el = time.perf_counter() - t0
-    p = 1.0 - eng.pool_weight(w)
-    proj = el * (1 - p) / p if p > 0 else float("inf")
+    W = eng.pool_weight(w)
+    rate = (W0 - W) / max(el - tw, 1e-9)
+    proj = W / rate if rate > 0 else float("inf")
+    W0, tw = W, el
     print(f"ta056 lb2 {el:7.1f} s: tree={st['tree']} pool={eng.size()} iters={st['iters']} "
-          f"-> {st['tree']/el/1e9:.3f} G nodes/s, explored {p:.3e} of the space, "
+          f"-> {st['tree']/el/1e9:.3f} G nodes/s, space left {W:.6e} (-{rate:.3e}/s), "
           f"projection {proj/3600:.3g} h on 1 GPU ({proj/3600/8:.3g} h on 8 at linear scaling)", flush=True)
     if eng.size() == 0:
         done = True

@@ -98,3 +98,27 @@ def test_lb2_bounds_large_buckets(inst):
     H = ops.require_gpu(0)
     gpu = H.pfsp_expand_probe(model.jobs, model.machines, list(model.native.p), 2, nodes, INT_MAX, 0, 0)
     assert np.array_equal(gpu, model.child_bounds_cpu(nodes))
+
+
+@pytest.mark.parametrize("machines", [2, 3, 7, 13, 17])
+@pytest.mark.parametrize("lb", [1, 2])
+def test_other_machine_counts_match_cpu(machines, lb):
+    # machine counts outside Taillard's 5/10/20 run in the next kernel bucket with
+    # zero-time padding machines: bounds, the LB2 expand path and whole trees must
+    # equal the host oracle's for the real instance
+    from dist_gpu_accelerated_tree_search_amd import solve_cpu, solve_gpu
+
+    model = PfspModel.synthetic(12, machines, 100 + machines, lb=lb)
+    nodes = random_nodes(12, 300, machines)
+    assert np.array_equal(model.child_bounds_gpu(nodes), model.child_bounds_cpu(nodes))
+    if lb == 2:
+        H = ops.require_gpu(0)
+        gpu = H.pfsp_expand_probe(12, machines, list(model.native.p), 2, nodes, INT_MAX, 0, 0)
+        assert np.array_equal(gpu, model.child_bounds_cpu(nodes))
+    ref = solve_cpu(model, ub=0)
+    got = solve_gpu(model, ub=0)
+    assert got.best == ref.best
+    bk = PfspModel.synthetic(12, machines, 100 + machines, lb=lb)
+    bk.best_known = ref.best  # -u 1 with the optimum: deterministic tree
+    r1, g1 = solve_cpu(bk, ub=1), solve_gpu(bk, ub=1)
+    assert (g1.tree, g1.sol, g1.best) == (r1.tree, r1.sol, r1.best)

@@ -11,18 +11,21 @@ pytestmark = pytest.mark.gpu
 GOLD14 = (2573652, 2648, 1377)
 
 
-@pytest.mark.parametrize("ub", [1, 0])
-def test_pinned_spill_and_refill_keep_the_tree(ub):
-    # a ring far too small for the pool: the bottom goes to pinned host blocks and
-    # comes back; with -u 1 the tree is deterministic, so no node may be lost
+@pytest.mark.parametrize("ub,frontier", [(1, 300_000), (1, 25), (0, 25)])
+def test_pinned_spill_and_refill_keep_the_tree(ub, frontier):
+    # a ring (2^19 nodes) far too small for the pool: the bottom goes to pinned host
+    # blocks (asynchronous D2H on the transfer stream) and comes back under the ring
+    # bottom (H2D ahead of need); with -u 1 the tree is deterministic, so no node may
+    # be lost or duplicated
     model = PfspModel(14, 1)
     eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1024, ring_bytes=1 << 20))
-    r = solve_engine(model, eng, ub=ub)
+    r = solve_engine(model, eng, ub=ub, m=frontier)
     st = eng.stats()
     assert r.best == 1377
     if ub == 1:
         assert (r.tree, r.sol) == GOLD14[:2]
-    assert st["spilled"] > 0 and st["refilled"] > 0 and st["pinned_bytes"] > 0, st
+    if frontier > 25:
+        assert st["spilled"] > 0 and st["refilled"] > 0 and st["pinned_bytes"] > 0, st
     assert st["host_nodes"] == 0 and st["device_nodes"] == 0
 
 
@@ -54,7 +57,7 @@ def test_export_import_between_engines_keeps_the_tree():
 def test_pop_push_roundtrip_preserves_nodes():
     model = PfspModel(14, 1)
     eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1024, ring_bytes=1 << 20))
-    nodes, _, _, best = model.warmup(model.initial_best(1), 100000)
+    nodes, _, _, best = model.warmup(model.initial_best(1), 400_000)
     eng.begin(nodes, int(best))  # more than half the ring: the rest goes to the pinned spill
     st = eng.stats()
     assert st["host_nodes"] > 0
