@@ -125,7 +125,7 @@ class DeviceEngine final : public IEngine {
     // pool spans a whole parent window (spec_min_). Queuing it earlier
     // (TTS_SPECULATE=1) was measured slower on ta014: an empty iteration still
     // costs ~4.5 us and two queued graphs are still ~13 us apart
-    // (profiles/r1f).
+    // (profiles/r1/r1f).
     {
       const char* e = std::getenv("TTS_SPECULATE");
       spec_min_ = (e && e[0] == '1') ? 1 : cfg_.max_parents;
@@ -581,7 +581,7 @@ class DeviceEngine final : public IEngine {
   // draining, more when the pool holds several parent windows.
   int pick_graph(size_t total, size_t extra) const {
     // right after begin(): one long replay (iters_first) — a graph boundary costs
-    // ~50 us of host sync + relaunch, an empty iteration ~4.5 us (profiles/r1f)
+    // ~50 us of host sync + relaunch, an empty iteration ~4.5 us (profiles/r1/r1f)
     size_t want = fresh_ ? std::max<size_t>(6, static_cast<size_t>(cfg_.iters_first)) : 6;
     while (want < static_cast<size_t>(cfg_.iters_large) && total >= (want / 6) * 2 * cfg_.max_parents) want *= 2;
     for (int i = static_cast<int>(ks_.size()) - 1; i >= 0; --i) {

@@ -166,12 +166,12 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   a.recs = upload_vec(img.recs);
   a.pinfo = upload_vec(img.pinfo);
   // wave-uniform pair walks measured 2.6x slower on ta056 (active children per chunk
-  // fill a fraction of a wave, profiles/r1af): dense (pair, child) tasks by default
+  // fill a fraction of a wave, profiles/r1/r1af): dense (pair, child) tasks by default
   a.lb2_wave = 0;
   if (const char* f = std::getenv("TTS_LB2_WAVE")) a.lb2_wave = std::atoi(f) != 0;  // A/B runs
   // B2 in rounds of pairs: ta056 (50x20) 0.060 -> 0.081 G nodes/s, ta020 (20x10)
   // 11.1 -> 8.0 ms, ta014 (20x10) even; ta010 (20x5, 10 pairs) 4.0 -> 4.6 ms
-  // (profiles/r1ak): on from 10 machines (45 pairs)
+  // (profiles/r1/r1ak): on from 10 machines (45 pairs)
   a.lb2_rounds = M >= 10 ? 1 : 0;
   if (const char* f = std::getenv("TTS_LB2_ROUNDS")) a.lb2_rounds = std::atoi(f) != 0;  // A/B runs
   // prefix/suffix walks (lb2_ps_walks): O(N) per (parent, pair) instead of per

@@ -384,7 +384,7 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 template <int NJ, int M, bool PACK>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 
-// Occupancy: the LB1 kernels are latency-bound (profiles/r1o), so the register
+// Occupancy: the LB1 kernels are latency-bound (profiles/r1/r1o), so the register
 // budget is capped for more resident waves (6 per SIMD for M <= 10: 80 VGPRs, no
 // spills); LB2 is bounded by its LDS footprint instead.
 template <int NJ, int M, int LBK>
@@ -423,7 +423,7 @@ struct PfspSmemLB2 {
   // lag:12}, in evaluation order (50 x 20: 38 KB)
   // records in LDS when they fit 32 KB (20 x 20: 30 KB); otherwise (50 x 20: 76 KB)
   // they are read from L2 (packing the leading pairs to 4 B in LDS measured no gain,
-  // profiles/r1ag)
+  // profiles/r1/r1ag)
   static constexpr bool kRecsInLds = C::P * NJ * 8 <= 32 * 1024;
   PfspNode<NJ> node[G::BP];
   uint32_t fr[G::BP][M];                  // parent front | remain << 16
@@ -458,8 +458,8 @@ struct PfspSmemLB2 {
 // scalar operands. The dense variant above spends a per-lane 8-B load (L2 latency:
 // the 50x20 tables are 76 KB, larger than L1) plus its unpacking on every step.
 // Cost: lanes past the active count idle (a chunk's active list is rarely a whole
-// number of waves). profiles/r1ae (dense: 60 % of wave cycles waiting); measured
-// 2.6x slower on ta056 (profiles/r1af: active children per chunk fill a fraction of
+// number of waves). profiles/r1/r1ae (dense: 60 % of wave cycles waiting); measured
+// 2.6x slower on ta056 (profiles/r1/r1af: active children per chunk fill a fraction of
 // a wave), so it is off by default (TTS_LB2_WAVE=1 turns it on).
 using kconst_u64 = const __attribute__((address_space(4))) unsigned long long;  // {x, y} of a uint2
 
@@ -862,7 +862,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
 // prefix and children loops are unrolled over all NJ positions and predicated on
 // the depth, so every job id is extracted with a static shift (v_bfe) — no LDS
 // node reads at all (the previous LDS node rows were read byte-wise by 64 lanes
-// with a 32-B stride: 8-way bank conflicts, profiles/r1_pmc). The only LDS
+// with a 32-B stride: 8-way bank conflicts, profiles/r1/r1_pmc). The only LDS
 // traffic is one padded p-table row per scheduled job and per child.
 template <int NJ>
 __device__ inline uint32_t node_byte(const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], int e) {

@@ -18,7 +18,7 @@
 //
 // Why not one atomic slot counter per chunk: measured on MI355X, 1024 returning
 // atomicAdds on one word per iteration serialise at ~88/us (~12 us per
-// iteration, profiles/r1_baseline); the prefix costs ~1 us of LDS work.
+// iteration, profiles/r1/r1_baseline); the prefix costs ~1 us of LDS work.
 #pragma once
 
 #include <cstddef>
@@ -172,7 +172,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // The slot and the control line are loaded together (one round trip). The
   // per-chunk counts are read once nch is known: reading the whole window's
   // counts speculatively in the same round trip made ta014 slower (0.32 -> 0.39
-  // ms, profiles/r1q: cold count lines), though ta008 gained 4 %.
+  // ms, profiles/r1/r1q: cold count lines), though ta008 gained 4 %.
   IterView v;
   v.S = ctl->slot[s_in].stack;
   v.nch_in = ctl->slot[s_in].nch;

@@ -33,7 +33,7 @@ class EngineOptions:
     ring_bytes: int = 16 << 30      # device pool capacity
     iters_small: int = 6
     iters_large: int = 48
-    iters_first: int = 18           # first graph replay after begin(): covers a 20-job tree (profiles/r1ac)
+    iters_first: int = 18           # first graph replay after begin(): covers a 20-job tree (profiles/r1/r1ac)
     use_graphs: bool = True
     cpu_batch: int = 4096           # CPU engine batch
     cpu_threads: int = 1
