@@ -168,6 +168,54 @@ PYBIND11_MODULE(_tts_cpu, m) {
       },
       py::arg("inst"), py::arg("lb"), py::arg("best"), py::arg("target"));
   m.def(
+      "lb2_child_profile",
+      [](const PfspInstance& in, U8 nodes, int best) {
+        // analysis helper: for every child of every node (LB2 work model of the expand
+        // kernel): LB1, the number of pairs in the learned order until the partial LB2
+        // exceeds best (P if never), and the full LB2
+        const std::vector<int> ord = lb2_pair_order(in);
+        std::vector<int> out;
+        with_pfsp_bucket(in.jobs, [&](auto nj) {
+          constexpr int NJ = decltype(nj)::value;
+          using Node = PfspNode<NJ>;
+          size_t n = 0;
+          const Node* p = array_nodes<Node>(nodes, n);
+          const int N = in.jobs;
+          for (size_t i = 0; i < n; ++i) {
+            const int d = p[i].depth;
+            for (int k = d; k < N; ++k) {
+              Node c = pfsp_child(p[i], k);
+              int front[64];
+              cpu_front(in, c.prmu, d + 1, front);
+              uint8_t sched[512] = {0};
+              for (int x = 0; x <= d; ++x) sched[c.prmu[x]] = 1;
+              int lb = 0, until = in.npairs;
+              for (int qi = 0; qi < in.npairs; ++qi) {
+                const int q = ord[qi];
+                const int m0 = in.pair_m0[q], m1 = in.pair_m1[q];
+                int t0 = front[m0], t1 = front[m1];
+                for (int r = 0; r < N; ++r) {
+                  const int j = in.johnson[static_cast<size_t>(q) * N + r];
+                  if (sched[j]) continue;
+                  t0 += in.pt(m0, j);
+                  t1 = std::max(t1, t0 + in.lags[static_cast<size_t>(q) * N + j]) + in.pt(m1, j);
+                }
+                lb = std::max(lb, std::max(t1 + in.min_tails[m1], t0 + in.min_tails[m0]));
+                if (lb >= best && until == in.npairs) until = qi + 1;
+              }
+              out.push_back(cpu_lb1(in, c.prmu, d + 1));
+              out.push_back(until);
+              out.push_back(lb);
+            }
+          }
+          return 0;
+        });
+        py::array_t<int> r({static_cast<py::ssize_t>(out.size() / 3), static_cast<py::ssize_t>(3)});
+        std::memcpy(r.mutable_data(), out.data(), out.size() * sizeof(int));
+        return r;
+      },
+      py::arg("inst"), py::arg("nodes"), py::arg("best"));
+  m.def(
       "tree_estimate",
       [](py::object problem, int best, unsigned long long probes, unsigned long long seed, int threads) {
         auto pack = [](const TreeEstimate& e) {

@@ -148,6 +148,14 @@ inline bool lb2_pack_wanted(const PfspInstance& in) {
   const char* f = std::getenv("TTS_LB2_PACK");
   return f && std::atoi(f) != 0 && lb2_records_pack(in);
 }
+// The LB2 kernel with prefix/suffix walks per (parent, pair) (LBK 4, lb2_ps_walks):
+// O(N) per (parent, pair) instead of per (child, pair), exact, but measured slower
+// than the per-child walks with the LB1 filter and early exit (ta056 0.082 -> 0.039
+// G nodes/s, ta010 4.3 -> 6.0 ms, profiles/r2/lb2_variants.md): TTS_LB2_PS=1 (A/B).
+inline bool lb2_ps_wanted() {
+  const char* f = std::getenv("TTS_LB2_PS");
+  return f && std::atoi(f) != 0;
+}
 
 template <class T>
 inline T* upload_vec(const std::vector<T>& v) {
@@ -174,14 +182,6 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   // (profiles/r1/r1ak): on from 10 machines (45 pairs)
   a.lb2_rounds = M >= 10 ? 1 : 0;
   if (const char* f = std::getenv("TTS_LB2_ROUNDS")) a.lb2_rounds = std::atoi(f) != 0;  // A/B runs
-  // prefix/suffix walks (lb2_ps_walks): O(N) per (parent, pair) instead of per
-  // (child, pair), but every live parent walks whole pair rounds. Measured slower
-  // than the per-child walks with the LB1 filter and early exit (ta056 0.081 -> 0.042
-  // G nodes/s, ta010 4.0 -> 7.4 ms, profiles/r2c: about one child per parent survives,
-  // and a survivor's full LB2 costs N steps per pair per-child vs 2N per parent):
-  // off by default, TTS_LB2_PS=1 turns it on
-  a.lb2_ps = 0;
-  if (const char* f = std::getenv("TTS_LB2_PS")) a.lb2_ps = std::atoi(f) != 0;
   auto eng = std::make_unique<DeviceEngine<PfspTraits<NJ, M, LBK>>>(cfg, a);
   eng->adopt(const_cast<uint16_t*>(a.ptab));
   eng->adopt(const_cast<uint2*>(a.recs));
@@ -272,7 +272,6 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
     a.pinfo = up(img.pinfo);
     a.dbg_off = up(offsets);
     a.dbg_lb = up(out);
-    a.lb2_ps = variant == 0;
     a.lb2_rounds = variant == 1;
     a.lb2_wave = variant == 3;
     size_t cap = 1;
@@ -294,8 +293,11 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
     pa.cap_mask = cap - 1;
     pa.max_parents = static_cast<int>(nchunks * G::BP);
     pa.max_chunks = static_cast<int>(nchunks);
-    hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), dim3(static_cast<unsigned>(std::min<size_t>(nchunks, 1024))),
-                       dim3(dev::kBlock), 0, 0, a, 0);
+    const dim3 grid(static_cast<unsigned>(std::min<size_t>(nchunks, 1024)));
+    if (variant == 0)
+      hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, 4>), grid, dim3(dev::kBlock), 0, 0, a, 0);
+    else
+      hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), grid, dim3(dev::kBlock), 0, 0, a, 0);
     TTS_HIP_CHECK(hipGetLastError());
     TTS_HIP_CHECK(hipDeviceSynchronize());
     TTS_HIP_CHECK(hipMemcpy(out.data(), a.dbg_lb, nb * sizeof(int), hipMemcpyDeviceToHost));
@@ -341,6 +343,7 @@ TTS_PFSP_DECLARE_BUCKET(500)
       if (lb != 2) return make_pfsp_engine_t<NJ, M, 1>(in, cfg);                                    \
       if constexpr (NJ == 50)                                                                        \
         if (lb2_pack_wanted(in)) return make_pfsp_engine_t<NJ, M, 3>(in, cfg);                       \
+      if (lb2_ps_wanted()) return make_pfsp_engine_t<NJ, M, 4>(in, cfg);                             \
       return make_pfsp_engine_t<NJ, M, 2>(in, cfg);                                                  \
     });                                                                                              \
   }                                                                                                  \

@@ -95,7 +95,6 @@ struct PfspArgs {
   // LB1 kernels' argument layout is unchanged)
   int lb2_wave;            // wave-uniform pair walks (1) or dense (pair, child) tasks (0)
   int lb2_rounds;          // B2 in rounds of pairs, re-compacting the children still below best
-  int lb2_ps;              // B2 as two prefix/suffix walks per (parent, pair) (default; see lb2_ps_walks)
   // element-wise probe of the expand kernel (tests): bound of every child of window
   // parent i at dbg_lb[dbg_off[i] + (k - depth)] (exact LB2 below best, else >= best)
   int* dbg_lb;
@@ -381,7 +380,7 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 
-template <int NJ, int M, bool PACK>
+template <int NJ, int M, bool PACK, bool PS>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 
 // Occupancy: the LB1 kernels are latency-bound (profiles/r1/r1o), so the register
@@ -391,9 +390,11 @@ template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
 void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
-    pfsp_expand_lb2<NJ, M, false>(a, t);
+    pfsp_expand_lb2<NJ, M, false, false>(a, t);
   else if constexpr (LBK == 3)
-    pfsp_expand_lb2<NJ, M, true>(a, t);
+    pfsp_expand_lb2<NJ, M, true, false>(a, t);  // records packed in LDS
+  else if constexpr (LBK == 4)
+    pfsp_expand_lb2<NJ, M, false, true>(a, t);  // prefix/suffix walks per (parent, pair)
   else if constexpr (sizeof(PfspNode<NJ>) == 32)
     pfsp_expand_lb1_small<NJ, M>(a, t);
   else
@@ -438,6 +439,8 @@ struct PfspSmemLB2 {
   int16_t alist[G::MAXCH];                // B2 rounds: active slots still below best
   int16_t jslot[G::BP][NJ];               // B2 prefix/suffix: (parent, job) -> active slot or -1
   uint8_t aparent[G::MAXCH];              // active slot -> chunk parent
+  uint8_t ajob[G::MAXCH];                 // active slot -> its job
+  u64 amask[G::BP];                       // jobs of the parent's children still below best (NJ <= 64)
   uint8_t palive[G::BP];                  // parent still has an active child below best
   uint8_t plist[G::BP];                   // ... compacted
   int npl;
@@ -518,18 +521,26 @@ __device__ inline void lb2_walks_wave(const PfspArgs<NJ, M>& a, S& sm, int nact,
 // it (LDS max). The value is the exact LB2 (all pairs, no early exit); a parent
 // leaves the task list once all its children exceed best (rounds of pairs in the
 // learned early-exit order), which changes no prune decision.
-template <int NJ, int M, class S>
+template <int NJ, int M, bool PACK, class S>
 __device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid, int nact, int best) {
   using G = PfspGeom<NJ, 2, M>;
   const int P = a.npairs;
   static_assert(G::BP <= kWave, "parent list is built by one wave");
+  constexpr bool kReg = NJ <= 64;  // one pass, the walk's w values in registers
   const int tid = threadIdx.x;
   const int N = a.jobs;
+  const uint2* recs = S::kRecsInLds ? sm.recs : a.recs;
   auto build_plist = [&]() {
-    if (tid < G::BP) sm.palive[tid] = 0;
+    if (tid < G::BP) {
+      sm.palive[tid] = 0;
+      sm.amask[tid] = 0;
+    }
     __syncthreads();
     for (int s = tid; s < nact; s += kBlock)
-      if (sm.lbv[s] < best) sm.palive[sm.aparent[s]] = 1;
+      if (sm.lbv[s] < best) {
+        sm.palive[sm.aparent[s]] = 1;
+        if constexpr (kReg) atomicOr(&sm.amask[sm.aparent[s]], 1ull << sm.ajob[s]);
+      }
     __syncthreads();
     if (tid < kWave) {
       const bool al = tid < nvalid && sm.palive[tid];
@@ -538,6 +549,22 @@ __device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid,
       if (tid == 0) sm.npl = __popcll(b);
     }
     __syncthreads();
+  };
+  // record r of pair slot qs: {job, p0, p1, lag}
+  auto rec = [&](int qs, uint2 pi, int r, int& j, int& p0, int& p1, int& lag) {
+    if constexpr (PACK) {
+      const uint32_t w = sm.rpk[qs * N + r];
+      j = static_cast<int>(w & 63u);
+      p0 = static_cast<int>((w >> 6) & 127u);
+      p1 = static_cast<int>((w >> 13) & 127u);
+      lag = static_cast<int>(w >> 20);
+    } else {
+      const uint2 rc = recs[static_cast<int>(pi.x >> 16) * N + r];
+      j = static_cast<int>(rc.x & 0xffff);
+      p0 = static_cast<int>(rc.x >> 16);
+      p1 = static_cast<int>(rc.y & 0xffff);
+      lag = static_cast<int>(rc.y >> 16);
+    }
   };
   build_plist();
   int q0 = 0, R = 8;
@@ -549,7 +576,8 @@ __device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid,
     for (int task = tid; task < ntask; task += kBlock) {
       const int qq = task / np;
       const int p = sm.plist[task - qq * np];
-      const uint2 pi = sm.pinfo[q0 + qq];
+      const int qs = q0 + qq;
+      const uint2 pi = sm.pinfo[qs];
       const int m0 = pi.x & 0xff, m1 = (pi.x >> 8) & 0xff;
       const int tail1 = static_cast<int>(pi.y >> 16);
       const int S0 = static_cast<int>(sm.fr[p][m0] >> 16), S1 = static_cast<int>(sm.fr[p][m1] >> 16);
@@ -557,38 +585,71 @@ __device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid,
       u64 msk[G::NW];
 #pragma unroll
       for (int w = 0; w < G::NW; ++w) msk[w] = sm.pmask[p][w];
-      const uint2* rq = a.recs + static_cast<int>(pi.x >> 16) * N;
       const int16_t* js = sm.jslot[p];
       const uint16_t* c0 = sm.cf[m0];
-      // forward: prefix maxima
-      int A = 0, Pb = 0, pre = INT_MIN / 4;
-#pragma unroll 4
-      for (int r = 0; r < N; ++r) {
-        const uint2 rc = rq[r];
-        const int j = static_cast<int>(rc.x & 0xffff);
-        if (job_in<G::NW>(msk, j)) continue;
-        const int p0 = static_cast<int>(rc.x >> 16), p1 = static_cast<int>(rc.y & 0xffff);
-        const int lag = static_cast<int>(rc.y >> 16);
-        A += p0;
-        const int sl = js[j];
-        if (sl >= 0) atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p1 + pre);
-        pre = max(pre, A - Pb + lag);
-        Pb += p1;
-      }
-      // backward: suffix maxima (A_j = S0 - p0 after j, Pb_j = S1 - p1 from j on)
-      int SA = 0, SB = 0, suf = INT_MIN / 4;
-#pragma unroll 4
-      for (int r = N - 1; r >= 0; --r) {
-        const uint2 rc = rq[r];
-        const int j = static_cast<int>(rc.x & 0xffff);
-        if (job_in<G::NW>(msk, j)) continue;
-        const int p0 = static_cast<int>(rc.x >> 16), p1 = static_cast<int>(rc.y & 0xffff);
-        const int lag = static_cast<int>(rc.y >> 16);
-        const int sl = js[j];
-        if (sl >= 0) atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p0 + suf);
-        SB += p1;
-        suf = max(suf, (S0 - SA) - (S1 - SB) + lag);
-        SA += p0;
+      if constexpr (kReg) {
+        // forward: prefix terms at the live children, w_j kept per position
+        const u64 am = sm.amask[p];
+        int wv[NJ];
+        u64 um = 0, cm = 0;  // positions in U / positions of live children
+        int A = 0, Pb = 0, pre = INT_MIN / 4;
+#pragma unroll
+        for (int r = 0; r < NJ; ++r) {
+          wv[r] = 0;
+          if (r < N) {
+            int j, p0, p1, lag;
+            rec(qs, pi, r, j, p0, p1, lag);
+            if (!((msk[0] >> j) & 1ull)) {
+              A += p0;
+              if ((am >> j) & 1ull) {
+                const int sl = js[j];
+                atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p1 + pre);
+                cm |= 1ull << r;
+              }
+              wv[r] = A - Pb + lag;
+              pre = max(pre, wv[r]);
+              Pb += p1;
+              um |= 1ull << r;
+            }
+          }
+        }
+        // backward over the kept values: suffix terms (records re-read only at live children)
+        int suf = INT_MIN / 4;
+#pragma unroll
+        for (int r = NJ - 1; r >= 0; --r) {
+          if ((cm >> r) & 1ull) {
+            int j, p0, p1, lag;
+            rec(qs, pi, r, j, p0, p1, lag);
+            const int sl = js[j];
+            atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p0 + suf);
+          }
+          if ((um >> r) & 1ull) suf = max(suf, wv[r]);
+        }
+      } else {
+        // forward: prefix maxima
+        int A = 0, Pb = 0, pre = INT_MIN / 4;
+        for (int r = 0; r < N; ++r) {
+          int j, p0, p1, lag;
+          rec(qs, pi, r, j, p0, p1, lag);
+          if (job_in<G::NW>(msk, j)) continue;
+          A += p0;
+          const int sl = js[j];
+          if (sl >= 0) atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p1 + pre);
+          pre = max(pre, A - Pb + lag);
+          Pb += p1;
+        }
+        // backward: suffix maxima (A_j = S0 - p0 after j, Pb_j = S1 - p1 from j on)
+        int SA = 0, SB = 0, suf = INT_MIN / 4;
+        for (int r = N - 1; r >= 0; --r) {
+          int j, p0, p1, lag;
+          rec(qs, pi, r, j, p0, p1, lag);
+          if (job_in<G::NW>(msk, j)) continue;
+          const int sl = js[j];
+          if (sl >= 0) atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p0 + suf);
+          SB += p1;
+          suf = max(suf, (S0 - SA) - (S1 - SB) + lag);
+          SA += p0;
+        }
       }
     }
     q0 += nq;
@@ -604,8 +665,28 @@ __device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid,
 // LDS (packed 4 B, PACK) or from `recs` (LDS or L2).
 template <int NJ, int M, bool PACK, class S>
 __device__ inline void lb2_johnson_walk(const S& sm, const uint2* recs, int qs, uint2 pi, int N,
-                                        const u64 (&msk)[PfspGeom<NJ, 2, M>::NW], int& t0, int& t1) {
+                                        const u64 (&msk)[PfspGeom<NJ, 2, M>::NW], int& t0, int& t1,
+                                        int uniform_ref = -1) {
   using G = PfspGeom<NJ, 2, M>;
+  if constexpr (!PACK && !S::kRecsInLds) {
+    // every active lane of the wave walks the same pair: the records are wave-uniform,
+    // read with scalar loads (constant address space, scalar cache) into SGPRs instead
+    // of one vector load per step (the tables are written before the first launch)
+    if (uniform_ref >= 0) {
+      kconst_u64* const rq = (kconst_u64*)(uintptr_t)recs + uniform_ref * N;
+#pragma unroll 8
+      for (int r = 0; r < N; ++r) {
+        const u64 rw = rq[r];
+        const uint32_t rx = static_cast<uint32_t>(rw), ry = static_cast<uint32_t>(rw >> 32);
+        const int n0 = t0 + static_cast<int>(rx >> 16);
+        const int n1 = max(t1, n0 + static_cast<int>(ry >> 16)) + static_cast<int>(ry & 0xffff);
+        const bool sched = job_in<G::NW>(msk, static_cast<int>(rx & 0xffff));
+        t0 = sched ? t0 : n0;
+        t1 = sched ? t1 : n1;
+      }
+      return;
+    }
+  }
   if constexpr (PACK) {
     const uint32_t* rq = sm.rpk + qs * N;
 #pragma unroll 4
@@ -631,7 +712,7 @@ __device__ inline void lb2_johnson_walk(const S& sm, const uint2* recs, int qs, 
   }
 }
 
-template <int NJ, int M, bool PACK>
+template <int NJ, int M, bool PACK, bool PS>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   using G = PfspGeom<NJ, 2, M>;
   using C = PfspConsts<M>;
@@ -719,15 +800,16 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
 #pragma unroll
         for (int w = 0; w < G::NW; ++w)
           sm.cm[slot][w] = sm.pmask[p][w] | (((job >> 6) == w) ? (1ull << (job & 63)) : 0ull);
-        sm.lbv[slot] = a.lb2_ps ? lb1c : 0;
+        sm.lbv[slot] = PS ? lb1c : 0;
         sm.aparent[slot] = static_cast<uint8_t>(p);
+        sm.ajob[slot] = static_cast<uint8_t>(job);
       }
       nact += cnt;
     }
     __syncthreads();
     // ---- B2: (pair, child) Johnson walks, pair-major ----
-    if (nact > 0 && a.lb2_ps) {
-      lb2_ps_walks<NJ, M>(a, sm, nvalid, nact, best);
+    if constexpr (PS) {
+      if (nact > 0) lb2_ps_walks<NJ, M, PACK>(a, sm, nvalid, nact, best);
     } else if (nact > 0 && a.lb2_wave) {
       lb2_walks_wave<NJ, M>(a, sm, __builtin_amdgcn_readfirstlane(nact), best);
     } else if (nact > 0 && a.lb2_rounds) {
@@ -746,13 +828,18 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         const int dq = kBlock / na, di = kBlock - dq * na;
         while (qq < nq) {
           const int ai = sm.alist[ii];
+          // wave-uniform pair among the lanes still in the loop?
+          const int qf = __builtin_amdgcn_readfirstlane(qq);
+          const int uref = __ballot(qq != qf) == 0
+                               ? __builtin_amdgcn_readfirstlane(static_cast<int>(sm.pinfo[q0 + qf].x >> 16))
+                               : -1;
           if (sm.lbv[ai] < best) {
             const uint2 pi = sm.pinfo[q0 + qq];
             int t0 = sm.cf[pi.x & 0xff][ai], t1 = sm.cf[(pi.x >> 8) & 0xff][ai];
             u64 msk[G::NW];
 #pragma unroll
             for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
-            lb2_johnson_walk<NJ, M, PACK>(sm, recs, q0 + qq, pi, N, msk, t0, t1);
+            lb2_johnson_walk<NJ, M, PACK>(sm, recs, q0 + qq, pi, N, msk, t0, t1, uref);
             atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
           }
           ii += di;
@@ -789,13 +876,16 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       int q = tid / nact, ai = tid - (tid / nact) * nact;
       const int dq = kBlock / nact, da = kBlock - dq * nact;
       while (q < P) {
+        const int qf = __builtin_amdgcn_readfirstlane(q);
+        const int uref =
+            __ballot(q != qf) == 0 ? __builtin_amdgcn_readfirstlane(static_cast<int>(sm.pinfo[qf].x >> 16)) : -1;
         if (sm.lbv[ai] < best) {
           const uint2 pi = sm.pinfo[q];
           int t0 = sm.cf[pi.x & 0xff][ai], t1 = sm.cf[(pi.x >> 8) & 0xff][ai];
           u64 msk[G::NW];
 #pragma unroll
           for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
-          lb2_johnson_walk<NJ, M, PACK>(sm, recs, q, pi, N, msk, t0, t1);
+          lb2_johnson_walk<NJ, M, PACK>(sm, recs, q, pi, N, msk, t0, t1, uref);
           atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
         }
         ai += da;

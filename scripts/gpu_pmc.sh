@@ -20,5 +20,9 @@ for spec in "$@"; do
       || { echo "pass $pass of $tag failed"; tail -5 "$out/$tag/p$pass.log"; exit 1; }
   done
   python3 scripts/pmc_summary.py "$out/$tag" pfsp_expand > "$out/$tag/summary.txt"
-  echo "== $tag"; grep -v "^  SQ" "$out/$tag/summary.txt" | head -20; tail -1 "$out/$tag/p1.log"
+  for pass in 1 2; do  # keep the per-kernel stats, drop the raw traces (gpurun_out must stay small)
+    find "$out/$tag/p$pass" -name "*kernel_stats.csv" -exec cp {} "$out/$tag/p${pass}_kernel_stats.csv" \; 2>/dev/null
+    rm -rf "$out/$tag/p$pass"
+  done
+  echo "== $tag"; cat "$out/$tag/summary.txt"; grep -v "^W20\|amdgpu.ids" "$out/$tag/p1.log" | tail -2
 done
