@@ -14,6 +14,7 @@
 #include <stdexcept>
 
 #include "../core/dist_rounds.hpp"
+#include "../core/dist_session.hpp"
 #include "../core/engine_api.hpp"
 #include "../core/runner.hpp"
 #include "../core/shm_control.hpp"
@@ -163,10 +164,117 @@ inline void bind_shm_control(py::module_& m) {
       .def_property_readonly("round_requested", &ShmControl::round_requested);
 }
 
+// ---- native rounds: options, control plane and callbacks from Python ----
+inline DistOptions dist_options_from(const py::dict& o) {
+  DistOptions opt;
+  auto get = [&](const char* k, auto& v) {
+    if (o.contains(k)) v = o[k].cast<std::remove_reference_t<decltype(v)>>();
+  };
+  get("needy_below", opt.needy_below);
+  get("donor_min", opt.donor_min);
+  get("steal_cap", opt.steal_cap);
+  get("slice_min", opt.slice_min);
+  get("slice_max", opt.slice_max);
+  get("intra", opt.intra);
+  get("inter", opt.inter);
+  get("local_world", opt.local_world);
+  get("early_rounds", opt.early_rounds);
+  get("max_rounds", opt.max_rounds);
+  get("checkpoint_every", opt.checkpoint_every);
+  get("watchdog_s", opt.watchdog_s);
+  get("watchdog_abort", opt.watchdog_abort);
+  get("fault_delay_us", opt.fault_delay_us);
+  get("fault_steal_fail_pct", opt.fault_steal_fail_pct);
+  get("fault_seed", opt.fault_seed);
+  return opt;
+}
+
+inline std::unique_ptr<RoundControl> round_control_from(uintptr_t shm_address, py::object allgather_fn, int rank,
+                                                        int world, double timeout_s) {
+  using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+  std::unique_ptr<RoundControl> ctl;
+  if (shm_address) {
+    ctl = std::make_unique<ShmRoundControl>(reinterpret_cast<ShmControl*>(shm_address), timeout_s);
+  } else {
+    if (allgather_fn.is_none()) throw std::invalid_argument("give a shm address or an allgather_fn");
+    ctl = std::make_unique<FnRoundControl>(rank, world, [allgather_fn, world](const int64_t* v, int n, int64_t* out) {
+      py::gil_scoped_acquire gil;
+      I64 a(static_cast<py::ssize_t>(n));
+      std::memcpy(a.mutable_data(), v, sizeof(int64_t) * static_cast<size_t>(n));
+      I64 r = allgather_fn(a).cast<I64>();
+      if (r.size() != static_cast<py::ssize_t>(world) * n) throw std::runtime_error("allgather_fn: wrong shape");
+      std::memcpy(out, r.data(), sizeof(int64_t) * static_cast<size_t>(world) * static_cast<size_t>(n));
+    });
+  }
+  if (ctl->rank() != rank || ctl->world() != world) throw std::invalid_argument("rank/world mismatch");
+  return ctl;
+}
+
+inline TransferFn transfer_from(py::object transfer_fn) {
+  return [transfer_fn](const Plan& p) -> std::pair<size_t, size_t> {
+    py::gil_scoped_acquire gil;
+    py::list l;
+    for (const auto& t : p) l.append(py::make_tuple(t.donor, t.receiver, t.n));
+    py::tuple r = transfer_fn(l).cast<py::tuple>();
+    return {r[0].cast<size_t>(), r[1].cast<size_t>()};
+  };
+}
+
+inline RoundHook hook_from(py::object round_hook) {
+  RoundHook hook;
+  if (!round_hook.is_none())
+    hook = [round_hook](unsigned long long r, int b, bool rep) {
+      py::gil_scoped_acquire gil;
+      round_hook(r, b, rep);
+    };
+  return hook;
+}
+
+// per-rank table as two arrays (one row per rank): cheap to hand to Python
+inline py::dict outcome_dict(const DistOutcome& out) {
+  const py::ssize_t W = static_cast<py::ssize_t>(out.tree.size());
+  py::array_t<int64_t> iv({W, static_cast<py::ssize_t>(11)});
+  py::array_t<double> fv({W, static_cast<py::ssize_t>(7)});
+  auto I = iv.mutable_unchecked<2>();
+  auto F = fv.mutable_unchecked<2>();
+  for (py::ssize_t r = 0; r < W; ++r) {
+    const unsigned long long cols[11] = {out.tree[r], out.sol[r], out.sent[r], out.received[r], out.transfers_in[r],
+                                         out.transfers_out[r], out.steals[r], out.success_steals[r],
+                                         out.idle_rounds[r], out.early_rounds[r], out.dropped[r]};
+    for (int k = 0; k < 11; ++k) I(r, k) = static_cast<int64_t>(cols[k]);
+    const double dc[7] = {out.t_run[r], out.t_comm[r], out.t_idle[r], out.t_termination[r], out.t_load_bal[r],
+                          out.t_memcpy[r], out.t_malloc[r]};
+    for (int k = 0; k < 7; ++k) F(r, k) = dc[k];
+  }
+  py::dict d;
+  d["best"] = out.best;
+  d["complete"] = out.complete;
+  d["rounds"] = out.rounds;
+  d["watchdog_events"] = out.watchdog_events;
+  d["counts"] = iv;  // tree sol sent received transfers_in transfers_out steals success_steals idle_rounds early_rounds dropped
+  d["times"] = fv;   // t_run t_comm t_idle t_termination t_load_bal t_memcpy t_malloc
+  return d;
+}
+
+// Builds the Step-1 warm-up of a Python model (PfspModel / QueensModel) in this module.
+using WarmupFactory = std::function<WarmupFn(py::object model)>;
+
+struct PyDistSession {
+  py::object engine_ref;  // keeps the engine alive
+  IEngine* e = nullptr;
+  std::unique_ptr<RoundControl> ctl;
+  DistOptions opt;
+  WarmupFn warm;
+  TransferFn xfer;
+  RoundHook hook;
+  size_t warm_target = 25, split_min = 1;
+  DistSolveResult last;
+};
+
 // dist_rounds(engine, shm_address | allgather_fn, rank, world, options, transfer_fn,
 //             round_hook, rounds0, timeout_s) -> dict (core/dist_rounds.hpp)
-inline void bind_dist_rounds(py::module_& m) {
-  using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+// DistSession(engine, model, ...).solve(best) -> one native cooperative solve (core/dist_session.hpp)
+inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory) {
   m.def(
       "plan_transfers",
       [](std::vector<int64_t> sizes, size_t needy_below, size_t donor_min, size_t cap, int local_world, bool intra,
@@ -182,88 +290,54 @@ inline void bind_dist_rounds(py::module_& m) {
       "dist_rounds",
       [](IEngine& e, uintptr_t shm_address, py::object allgather_fn, int rank, int world, py::dict o,
          py::object transfer_fn, py::object round_hook, unsigned long long rounds0, double timeout_s) {
-        DistOptions opt;
-        auto get = [&](const char* k, auto& v) {
-          if (o.contains(k)) v = o[k].cast<std::remove_reference_t<decltype(v)>>();
-        };
-        get("needy_below", opt.needy_below);
-        get("donor_min", opt.donor_min);
-        get("steal_cap", opt.steal_cap);
-        get("slice_min", opt.slice_min);
-        get("slice_max", opt.slice_max);
-        get("intra", opt.intra);
-        get("inter", opt.inter);
-        get("local_world", opt.local_world);
-        get("early_rounds", opt.early_rounds);
-        get("max_rounds", opt.max_rounds);
-        get("checkpoint_every", opt.checkpoint_every);
-        get("watchdog_s", opt.watchdog_s);
-        get("watchdog_abort", opt.watchdog_abort);
-        get("fault_delay_us", opt.fault_delay_us);
-        get("fault_steal_fail_pct", opt.fault_steal_fail_pct);
-        get("fault_seed", opt.fault_seed);
-        std::unique_ptr<RoundControl> ctl;
-        if (shm_address) {
-          ctl = std::make_unique<ShmRoundControl>(reinterpret_cast<ShmControl*>(shm_address), timeout_s);
-        } else {
-          if (allgather_fn.is_none()) throw std::invalid_argument("dist_rounds: give a shm address or an allgather_fn");
-          ctl = std::make_unique<FnRoundControl>(rank, world, [allgather_fn, world](const int64_t* v, int n, int64_t* out) {
-            py::gil_scoped_acquire gil;
-            I64 a(static_cast<py::ssize_t>(n));
-            std::memcpy(a.mutable_data(), v, sizeof(int64_t) * static_cast<size_t>(n));
-            I64 r = allgather_fn(a).cast<I64>();
-            if (r.size() != static_cast<py::ssize_t>(world) * n) throw std::runtime_error("allgather_fn: wrong shape");
-            std::memcpy(out, r.data(), sizeof(int64_t) * static_cast<size_t>(world) * static_cast<size_t>(n));
-          });
-        }
-        if (ctl->rank() != rank || ctl->world() != world) throw std::invalid_argument("dist_rounds: rank/world mismatch");
-        TransferFn xfer = [transfer_fn](const Plan& p) -> std::pair<size_t, size_t> {
-          py::gil_scoped_acquire gil;
-          py::list l;
-          for (const auto& t : p) l.append(py::make_tuple(t.donor, t.receiver, t.n));
-          py::tuple r = transfer_fn(l).cast<py::tuple>();
-          return {r[0].cast<size_t>(), r[1].cast<size_t>()};
-        };
-        RoundHook hook;
-        if (!round_hook.is_none())
-          hook = [round_hook](unsigned long long r, int b, bool rep) {
-            py::gil_scoped_acquire gil;
-            round_hook(r, b, rep);
-          };
+        const DistOptions opt = dist_options_from(o);
+        auto ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s);
+        const TransferFn xfer = transfer_from(transfer_fn);
+        const RoundHook hook = hook_from(round_hook);
         DistOutcome out;
         {
           py::gil_scoped_release nogil;
           out = run_dist_rounds(e, *ctl, opt, xfer, hook, rounds0);
         }
-        // per-rank table as two arrays (one row per rank): cheap to hand to Python
-        const py::ssize_t W = static_cast<py::ssize_t>(out.tree.size());
-        py::array_t<int64_t> iv({W, static_cast<py::ssize_t>(11)});
-        py::array_t<double> fv({W, static_cast<py::ssize_t>(7)});
-        auto I = iv.mutable_unchecked<2>();
-        auto F = fv.mutable_unchecked<2>();
-        for (py::ssize_t r = 0; r < W; ++r) {
-          const unsigned long long cols[11] = {out.tree[r], out.sol[r], out.sent[r], out.received[r],
-                                               out.transfers_in[r], out.transfers_out[r], out.steals[r],
-                                               out.success_steals[r], out.idle_rounds[r], out.early_rounds[r],
-                                               out.dropped[r]};
-          for (int k = 0; k < 11; ++k) I(r, k) = static_cast<int64_t>(cols[k]);
-          const double dc[7] = {out.t_run[r], out.t_comm[r], out.t_idle[r], out.t_termination[r], out.t_load_bal[r],
-                                out.t_memcpy[r], out.t_malloc[r]};
-          for (int k = 0; k < 7; ++k) F(r, k) = dc[k];
-        }
-        py::dict d;
-        d["best"] = out.best;
-        d["complete"] = out.complete;
-        d["rounds"] = out.rounds;
-        d["watchdog_events"] = out.watchdog_events;
-        d["counts"] = iv;  // tree sol sent received transfers_in transfers_out steals success_steals idle_rounds early_rounds dropped
-        d["times"] = fv;   // t_run t_comm t_idle t_termination t_load_bal t_memcpy t_malloc
-        return d;
+        return outcome_dict(out);
       },
       py::arg("engine"), py::arg("shm_address"), py::arg("allgather_fn"), py::arg("rank"), py::arg("world"),
       py::arg("options"), py::arg("transfer_fn"), py::arg("round_hook") = py::none(), py::arg("rounds0") = 0,
       py::arg("timeout_s") = 1800.0,
       "Native lock-step rounds of a multi-rank solve until every pool is empty (or max_rounds).");
+  py::class_<PyDistSession>(m, "DistSession", py::module_local())
+      .def(py::init([warmup_factory](py::object engine, py::object model, uintptr_t shm_address, py::object allgather_fn,
+                                     int rank, int world, py::dict o, py::object transfer_fn, py::object round_hook,
+                                     size_t warm_target, size_t split_min, double timeout_s) {
+             auto s = std::make_unique<PyDistSession>();
+             s->engine_ref = engine;
+             s->e = engine.cast<IEngine*>();
+             s->ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s);
+             s->opt = dist_options_from(o);
+             s->warm = warmup_factory(model);
+             s->xfer = transfer_from(transfer_fn);
+             s->hook = hook_from(round_hook);
+             s->warm_target = warm_target;
+             s->split_min = split_min;
+             return s;
+           }),
+           py::arg("engine"), py::arg("model"), py::arg("shm_address"), py::arg("allgather_fn"), py::arg("rank"),
+           py::arg("world"), py::arg("options"), py::arg("transfer_fn"), py::arg("round_hook") = py::none(),
+           py::arg("warm_target") = 25, py::arg("split_min") = 1, py::arg("timeout_s") = 1800.0)
+      .def(
+          "solve",
+          [](PyDistSession& s, int best) {
+            {
+              py::gil_scoped_release nogil;
+              s.last = dist_solve_split(*s.e, *s.ctl, s.opt, s.warm, best, s.warm_target, s.split_min, s.xfer, s.hook);
+            }
+            const auto& r = s.last;
+            return py::make_tuple(r.best, r.tree, r.sol, r.rounds, r.complete, r.t_init, r.t_search, r.elapsed);
+          },
+          py::arg("best"),
+          "One cooperative solve: (best, tree, sol, rounds, complete, t_init, t_search, elapsed), global values.")
+      .def("outcome", [](const PyDistSession& s) { return outcome_dict(s.last.outcome); },
+           "Per-rank counters and timers of the last solve (same layout as dist_rounds).");
 }
 
 // run_workers(engines, initial_nodes, best, ...) -> {"best": int, "workers": [dict]}

@@ -313,5 +313,15 @@ PYBIND11_MODULE(_tts_cpu, m) {
       py::arg("N"), py::arg("G") = 1, py::arg("batch") = 4096, py::arg("threads") = 1);
 
   bind_shm_control(m);
-  bind_dist_rounds(m);
+  bind_dist_rounds(m, [](py::object model) -> WarmupFn {
+    if (py::hasattr(model, "native")) {
+      auto inst = std::make_shared<PfspInstance>(model.attr("native").cast<const PfspInstance&>());
+      const int lb = model.attr("host_lb").cast<int>();
+      return with_pfsp_bucket(inst->jobs, [&](auto nj) -> WarmupFn {
+        constexpr int NJ = decltype(nj)::value;
+        return make_warmup(inst, PfspProblem<NJ>(*inst, lb));
+      });
+    }
+    return make_warmup(nullptr, QueensProblem(model.attr("N").cast<int>(), model.attr("G").cast<int>()));
+  });
 }

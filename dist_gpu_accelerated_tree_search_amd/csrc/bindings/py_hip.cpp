@@ -42,7 +42,19 @@ PYBIND11_MODULE(_tts_hip, m) {
   m.doc() = "gfx950 (MI355X) device engines: device-resident pools, fused bound/prune/compact kernels, hipGraphs.";
   bind_engine(m);
   bind_shm_control(m);
-  bind_dist_rounds(m);
+  bind_dist_rounds(m, [](py::object model) -> WarmupFn {
+    if (py::hasattr(model, "native")) {
+      auto inst = std::make_shared<PfspInstance>(make_instance(model.attr("jobs").cast<int>(),
+                                                               model.attr("machines").cast<int>(),
+                                                               model.attr("native").attr("p").cast<std::vector<int>>()));
+      const int lb = model.attr("host_lb").cast<int>();
+      return with_pfsp_bucket(inst->jobs, [&](auto nj) -> WarmupFn {
+        constexpr int NJ = decltype(nj)::value;
+        return make_warmup(inst, PfspProblem<NJ>(*inst, lb));
+      });
+    }
+    return make_warmup(nullptr, QueensProblem(model.attr("N").cast<int>(), model.attr("G").cast<int>()));
+  });
   bind_runner(
       m, []() -> std::unique_ptr<DeviceStaging> { return std::make_unique<HipStaging>(); }, &device_cpus);
   if (!std::getenv("TTS_NO_ROCTX")) install_roctx_hooks();

@@ -1,0 +1,83 @@
+// One native call per cooperative solve (the default multi-rank Step 1): host warm-up,
+// in-search rank split, native rounds, final reductions — no Python between them.
+//
+// Parity: ref pfsp_dist_multigpu_cuda.c:142-905 (Step 1 redundant BFS on every rank,
+// Step 2 rounds, reductions). The Python runtime (parallel/runtime.py) keeps the other
+// Step-1 variants (host round-robin share, engine warm-up, resume) and calls
+// run_dist_rounds directly; this session is what bench.py times at N > 1, so a solve
+// of a 0.3-ms tree does not pay tens of microseconds of interpreter work per rank.
+#pragma once
+
+#include <chrono>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <vector>
+
+#include "dist_rounds.hpp"
+#include "search_cpu.hpp"
+
+namespace tts {
+
+struct WarmupResult {
+  std::vector<uint8_t> nodes;  // n nodes in the engine's layout
+  size_t n = 0;
+  unsigned long long tree = 0, sol = 0;
+  int best = 0;
+};
+using WarmupFn = std::function<WarmupResult(int best, size_t target)>;
+
+// Step 1 of `prob` (host breadth-first to `target` nodes); `keep` holds what the
+// problem refers to (the instance) alive.
+template <class Problem>
+WarmupFn make_warmup(std::shared_ptr<const void> keep, Problem prob) {
+  return [keep, prob](int best, size_t target) {
+    using Node = typename Problem::Node;
+    Pool<Node> pool;
+    pool.push_back_free(prob.root());
+    WarmupResult r;
+    r.best = best;
+    bfs_warmup(prob, pool, target, r.best, r.tree, r.sol);
+    r.n = pool.size();
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(pool.data());
+    r.nodes.assign(p, p + r.n * sizeof(Node));
+    return r;
+  };
+}
+
+struct DistSolveResult {
+  int best = 0;
+  unsigned long long tree = 0, sol = 0, rounds = 0;
+  bool complete = true;
+  double t_init = 0, t_search = 0, elapsed = 0;
+  DistOutcome outcome;
+};
+
+// Every rank: the same warm-up to `warm_target` nodes, the split armed at `split_min`
+// pool nodes (IEngine::set_split), the rounds, then global counts (Step-1 counts once).
+inline DistSolveResult dist_solve_split(IEngine& e, RoundControl& ctl, const DistOptions& o, const WarmupFn& warm,
+                                        int best, size_t warm_target, size_t split_min, const TransferFn& xfer,
+                                        const RoundHook& hook) {
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  WarmupResult w = warm(best, warm_target);
+  if (ctl.world() > 1) e.set_split(ctl.rank(), ctl.world(), split_min);
+  e.begin(w.nodes.data(), w.n, w.best);
+  const auto t1 = clock::now();
+  DistSolveResult r;
+  r.outcome = run_dist_rounds(e, ctl, o, xfer, hook, 0);
+  const auto t2 = clock::now();
+  r.tree = w.tree;
+  r.sol = w.sol;
+  for (auto x : r.outcome.tree) r.tree += x;
+  for (auto x : r.outcome.sol) r.sol += x;
+  r.best = std::min(r.outcome.best, w.best);
+  r.rounds = r.outcome.rounds;
+  r.complete = r.outcome.complete;
+  r.t_init = std::chrono::duration<double>(t1 - t0).count();
+  r.t_search = std::chrono::duration<double>(t2 - t1).count();
+  r.elapsed = std::chrono::duration<double>(t2 - t0).count();
+  return r;
+}
+
+}  // namespace tts

@@ -287,3 +287,50 @@ class RankTable(list):
     def __repr__(self):
         self._fill()
         return super().__repr__()
+
+
+class DistSolver:
+    """Reusable native session for repeated cooperative solves with the default Step 1
+    (same host warm-up on every rank + in-search split; csrc/core/dist_session.hpp):
+    one native call per solve — warm-up, split, rounds and final reductions run without
+    the interpreter, which is what a 0.3-ms tree needs at N > 1 (bench.py). Per-rank
+    statistics of the last solve: `last_outcome()` / `result(...).workers`."""
+
+    def __init__(self, model, engine, comm: Comm, cfg: DistConfig | None = None, window: int | None = None):
+        cfg = cfg or DistConfig()
+        if cfg.checkpoint_dir or cfg.max_rounds or cfg.resume or cfg.engine_warmup or cfg.start_on is not None:
+            raise ValueError("DistSolver runs the default Step 1 only; use distributed_solve for the other modes")
+        self.model, self.engine, self.comm, self.cfg = model, engine, comm, cfg
+        self.needy, self.donor, opts = _native_options(cfg, engine, comm, window)
+        native = type(engine).__module__.rsplit(".", 1)[-1]
+        mod = ops.hip() if native == "_tts_hip" else ops.cpu()
+        shm = comm.control_address(mod)
+        world = comm.world
+        split = cfg.split and world > 1
+        self._s = mod.DistSession(engine, model, shm, None if shm else comm.allgather_i64, comm.rank, world, opts,
+                                  lambda plan: comm.execute_transfers(plan, engine, model.node_bytes), None,
+                                  int(cfg.m if split or world == 1 else world * cfg.init_per_rank),
+                                  int(cfg.split_per_rank * world), float(comm.timeout_s))
+
+    def solve_raw(self, ub: int = 1) -> tuple:
+        """(best, tree, sol, rounds, complete, t_init, t_search, elapsed), global values."""
+        return self._s.solve(int(self.model.initial_best(ub)))
+
+    def solve(self, ub: int = 1) -> SolveResult:
+        best, tree, sol, rounds, complete, t_init, t_search, elapsed = self.solve_raw(ub)
+        return self.result(best, tree, sol, rounds, complete, t_init, t_search, elapsed)
+
+    def last_outcome(self) -> dict:
+        return self._s.outcome()
+
+    def result(self, best, tree, sol, rounds, complete, t_init, t_search, elapsed) -> SolveResult:
+        out = self._s.outcome()
+        cnt, tms = out["counts"], out["times"]
+        return SolveResult(best=int(best), tree=int(tree), sol=int(sol), elapsed=elapsed, t_init=t_init,
+                           t_search=t_search, t_tail=0.0, workers=RankTable(cnt, tms),
+                           extra={"rounds": int(rounds), "sent_nodes": cnt[:, 2].tolist(),
+                                  "received_nodes": cnt[:, 3].tolist(), "world": self.comm.world,
+                                  "complete": bool(complete), "dropped_transfers": int(cnt[:, 10].sum()),
+                                  "watchdog_events": int(out["watchdog_events"]),
+                                  "early_rounds": cnt[:, 9].tolist(), "needy_below": self.needy,
+                                  "donor_min": self.donor})

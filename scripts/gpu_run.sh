@@ -1,6 +1,6 @@
 #!/bin/bash
 # Parameterised GPU-box session: scripts/gpu_run.sh <out-dir> <step>...
-# steps: tests[:<pytest -k expr>] | bench1 | bench2shared | smoke | lb2:<ta056 seconds>
+# steps: tests[:<pytest -k expr>] | bench1 | bench2shared | smoke | lb2:<ta056 seconds>[@ENV=V,...] | trace:<workload>
 # Every step runs under its own timeout; the session stops at the first failure.
 set -o pipefail
 out=gpurun_out/$1; shift
@@ -29,6 +29,13 @@ for step in "$@"; do
         timeout -k 10 $((secs + 240)) python -u scripts/lb2_probe.py "$secs" 10 > "$out/$tag.txt" 2>&1 ) \
         || { tail -20 "$out/$tag.txt"; exit 1; }
       cat "$out/$tag.txt" ;;
+    trace:*)  # trace:<workload>: kernel + memory-copy trace, copy/kernel overlap summary
+      wl="${step#trace:}"
+      ( cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
+        timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace -d "$out/trace_$wl" -o run --output-format csv \
+          -- python3 scripts/profile_workload.py "$wl" > "$out/trace_$wl.log" 2>&1 ) || { tail -20 "$out/trace_$wl.log"; exit 1; }
+      python3 scripts/overlap.py "$out/trace_$wl" > "$out/overlap_$wl.txt"; rm -rf "$out/trace_$wl"
+      grep -v "^W20\|^E20\|amdgpu.ids" "$out/trace_$wl.log" | tail -2; cat "$out/overlap_$wl.txt" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
         || { tail -20 "$out/smoke.log"; exit 1; }

@@ -21,6 +21,15 @@ def test_gpu_ranks_golden(world):
         assert (r["tree"], r["sol"], r["best"]) == (2573652, 2648, 1377)
 
 
+def test_gpu_native_session():
+    # bench.py's N > 1 path: runtime.DistSolver (one native call per solve) with GPU engines
+    spec = {"problem": "pfsp", "inst": 14, "lb": 1, "backend": "gpu", "comm": "gloo", "device": 0, "session": True,
+            "repeat": 3, "engine": {"ring_bytes": 1 << 28, "max_parents": 1 << 16}}
+    res = spawn_local(2, solve_rank, (spec,), timeout=600)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == (2573652, 2648, 1377)
+
+
 def test_gpu_ranks_queens():
     spec = {"problem": "nqueens", "N": 13, "backend": "gpu", "comm": "gloo", "device": 0,
             "engine": {"ring_bytes": 1 << 28, "max_parents": 1 << 12}, "dist": {"slice_min_s": 0.0001}}
