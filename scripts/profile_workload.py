@@ -42,9 +42,9 @@ elif which == "ta021":  # LB1_d 20x20 (BASELINE 8-GPU config), time-boxed
     print(which, st["tree"], st["iters"], "pool", eng.size())
     raise SystemExit(0)
 elif which == "spill":  # pinned spill/refill on a small ring (copies overlapping graph replays)
-    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 12, ring_bytes=1 << 24))
+    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=1 << 20))
     for _ in range(3):
-        r = solve_engine(m, eng, m=1_500_000)
+        r = solve_engine(m, eng, m=300_000)
     st = eng.stats()
     print(which, "spilled", st["spilled"], "refilled", st["refilled"], "pinned MB", st["pinned_bytes"] >> 20)
 elif which == "queens":
