@@ -304,6 +304,7 @@ class DeviceEngine final : public IEngine {
     for (;;) {
       // ---- nothing in flight on the compute stream: the host shadow is the device state ----
       check_overflow();
+      commit_spill_ahead();
       poll_transfers();
       size_t total = dev_total();
       const size_t all = total + spill_.size() + refill_n_;
@@ -312,10 +313,12 @@ class DeviceEngine final : public IEngine {
       if (max_launches >= 0 && launches >= max_launches) break;
       if (max_seconds > 0 && elapsed() >= max_seconds) break;
       if (hook_ && hook_(all)) break;
-      // refill ahead of need from the pinned spill (overlaps the next replays)
-      if (refill_n_ == 0 && !spill_.empty() && total < 4 * cfg_.max_parents) {
+      // refill ahead of need from the pinned spill, one pinned block at a time, while
+      // the device still holds work for the next replays to overlap the copy with
+      const size_t low = std::max(4 * cfg_.max_parents, spill_.block_nodes() / 2);
+      if (refill_n_ == 0 && !spill_.empty() && total < low) {
         normalize();
-        start_refill(4 * cfg_.max_parents);
+        start_refill(std::max(4 * cfg_.max_parents, spill_.block_nodes()));
         upload_ctl();
         total = dev_total();
       }
@@ -345,6 +348,7 @@ class DeviceEngine final : public IEngine {
       }
       launch_graph(gi);
       ++launches;
+      start_spill_ahead();
       // ---- pipelined replays: while one graph runs, queue the next one if the
       // last known pool spans at least one parent window and the worst-case
       // growth of both fits; then read the older graph's mirror. Hides the host
@@ -657,6 +661,7 @@ class DeviceEngine final : public IEngine {
   // Host shadow current and every asynchronous spill copy folded in.
   void settle() {
     sync_ctl();
+    commit_spill_ahead();
     if (refill_n_) finish_refill();
     poll_transfers();
   }
@@ -696,18 +701,54 @@ class DeviceEngine final : public IEngine {
     h_ctl_->slot[0].stack -= n;
     stats_.spilled += n;
   }
+  // Spill ahead, overlapped with the replays. Past 3/4 of the ring, right after a graph
+  // launch, the oldest nodes above half the ring start their D2H on the transfer
+  // stream. The running graphs cannot touch them: a graph consumes at most its
+  // iterations x window parents from the top, and two graphs in flight take far
+  // less than the half ring kept (the ring holds >= 16 windows of children per
+  // window parent), so the copy reads nodes no replay reads or writes. They leave
+  // the stack (and stay reserved until the copy is done) once the replays have
+  // completed (commit_spill_ahead, nothing in flight).
+  void start_spill_ahead() {
+    if (ahead_n_ || !resv_.empty() || dev_stack() <= cap_ / 4 * 3) return;
+    const size_t keep = std::max(cap_ / 2, 2 * static_cast<size_t>(ks_.back() + 1) * cfg_.max_parents);
+    if (dev_stack() <= keep) return;
+    const size_t n = dev_stack() - keep;
+    const size_t start = h_ctl_->bot & (cap_ - 1);
+    const size_t first = std::min(n, cap_ - start);
+    auto reserve = [&](hipEvent_t ev, size_t k) { ahead_.emplace_back(ev, k); };
+    spill_.push_from_device(d_ring_ + start, first, xfer_, reserve);
+    if (first < n) spill_.push_from_device(d_ring_, n - first, xfer_, reserve);
+    ahead_n_ = n;
+  }
+  void commit_spill_ahead() {
+    if (!ahead_n_) return;
+    h_ctl_->bot = (h_ctl_->bot + ahead_n_) & (cap_ - 1);
+    h_ctl_->slot[0].stack -= ahead_n_;
+    for (auto& r : ahead_) {
+      resv_.push_back(r);
+      reserved_ += r.second;
+    }
+    ahead_.clear();
+    stats_.spilled += ahead_n_;
+    ahead_n_ = 0;
+    upload_ctl();
+  }
+
   // Asynchronous H2D of up to `want` of the newest spilled nodes under the ring
   // bottom (one pinned block at most), on the transfer stream. The nodes join the
   // pool when the copy has completed (fold_refill). Returns false without room.
   bool start_refill(size_t want) {
     if (refill_n_ || spill_.empty() || want == 0) return false;
-    // like push_host: the device part stays within half the ring (the rest is
-    // growth room for the replays, checked by pick_graph)
+    // like push_host: the device part stays within half the ring, and the smallest
+    // graph must still fit afterwards (else refills and spills would alternate)
     const size_t used = dev_total() + reserved_;
-    if (used >= cap_ / 2) return false;
+    const size_t growth = static_cast<size_t>(ks_.front() + 1) * buf_nodes_;
+    const size_t limit = std::min(cap_ / 2, cap_ > growth ? cap_ - growth : 0);
+    if (used >= limit) return false;
     const size_t b0 = h_ctl_->bot & (cap_ - 1);
     // one pinned block at most, contiguous under the ring bottom
-    const size_t k = std::min({want, spill_.top_count(), cap_ / 2 - used, b0 ? b0 : cap_});
+    const size_t k = std::min({want, spill_.top_count(), limit - used, b0 ? b0 : cap_});
     if (k == 0) return false;
     Node* dst = d_ring_ + ((b0 + cap_ - k) & (cap_ - 1));
     if (spill_.pop_to_device(dst, k, xfer_, &refill_ev_) != k) throw std::logic_error("pinned spill: short refill");
@@ -790,6 +831,8 @@ class DeviceEngine final : public IEngine {
   std::deque<std::pair<hipEvent_t, size_t>> resv_;     // spill copies in flight (ring span reserved)
   size_t reserved_ = 0;                                // ring nodes reserved by copies in flight
   size_t refill_n_ = 0;                                // nodes of the refill in flight
+  size_t ahead_n_ = 0;                                 // spill-ahead copy in flight, not yet committed
+  std::deque<std::pair<hipEvent_t, size_t>> ahead_;
   hipEvent_t refill_ev_ = nullptr;
   ProgressHook hook_;
   int next_mirror_ = 0;

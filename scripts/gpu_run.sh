@@ -32,7 +32,7 @@ for step in "$@"; do
     trace:*)  # trace:<workload>: kernel + memory-copy trace, copy/kernel overlap summary
       wl="${step#trace:}"
       ( cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
-        timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace -d "$out/trace_$wl" -o run --output-format csv \
+        timeout -k 10 150 rocprofv3 --kernel-trace --memory-copy-trace -d "$out/trace_$wl" -o run --output-format csv \
           -- python3 scripts/profile_workload.py "$wl" > "$out/trace_$wl.log" 2>&1 ) || { tail -20 "$out/trace_$wl.log"; exit 1; }
       python3 scripts/overlap.py "$out/trace_$wl" > "$out/overlap_$wl.txt"; rm -rf "$out/trace_$wl"
       grep -v "^W20\|^E20\|amdgpu.ids" "$out/trace_$wl.log" | tail -2; cat "$out/overlap_$wl.txt" ;;

@@ -41,12 +41,14 @@ elif which == "ta021":  # LB1_d 20x20 (BASELINE 8-GPU config), time-boxed
     st = eng.stats()
     print(which, st["tree"], st["iters"], "pool", eng.size())
     raise SystemExit(0)
-elif which == "spill":  # pinned spill/refill on a small ring (copies overlapping graph replays)
-    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=1 << 20))
-    for _ in range(3):
-        r = solve_engine(m, eng, m=300_000)
+elif which == "spill":  # pinned spill/refill: a ring smaller than the pool (copies overlapping replays)
+    m = PfspModel(14, 1); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=256, ring_bytes=1 << 20))
+    for _ in range(2):
+        r = solve_engine(m, eng, m=200_000)
     st = eng.stats()
-    print(which, "spilled", st["spilled"], "refilled", st["refilled"], "pinned MB", st["pinned_bytes"] >> 20)
+    assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377), (r.tree, r.sol, r.best)
+    print(which, "ta014 spilled", st["spilled"], "refilled", st["refilled"], "pinned MB", st["pinned_bytes"] >> 20,
+          "capacity", st["capacity"], f"{r.elapsed * 1e3:.1f} ms")
 elif which == "queens":
     m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=32 << 30))
     r = solve_engine(m, eng)

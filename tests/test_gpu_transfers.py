@@ -11,14 +11,15 @@ pytestmark = pytest.mark.gpu
 GOLD14 = (2573652, 2648, 1377)
 
 
-@pytest.mark.parametrize("ub,frontier", [(1, 300_000), (1, 25), (0, 25)])
-def test_pinned_spill_and_refill_keep_the_tree(ub, frontier):
+@pytest.mark.parametrize("ub,frontier,window", [(1, 300_000, 1024), (1, 25, 1024), (0, 25, 1024), (1, 200_000, 256)])
+def test_pinned_spill_and_refill_keep_the_tree(ub, frontier, window):
     # a ring (2^19 nodes) far too small for the pool: the bottom goes to pinned host
     # blocks (asynchronous D2H on the transfer stream) and comes back under the ring
     # bottom (H2D ahead of need); with -u 1 the tree is deterministic, so no node may
     # be lost or duplicated
     model = PfspModel(14, 1)
-    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1024, ring_bytes=1 << 20))
+    # (window 256: a graph's growth is over half the ring, refills must leave room for it)
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=window, ring_bytes=1 << 20))
     r = solve_engine(model, eng, ub=ub, m=frontier)
     st = eng.stats()
     assert r.best == 1377

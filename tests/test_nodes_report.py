@@ -84,3 +84,26 @@ def test_csv_formats(tmp_path):
     report.write_dist_multi_gpu_csv(str(d), 14, 1, 1, 0, 1, 2, 1377, 25, 50000, 5000, 1.0, 12, 1, w, [3, 4], [0.1, 0.2])
     row = d.read_text().splitlines()[1]
     assert row.startswith("14,1,0,2,1,1,1377,25,50000,5000,1.0000,12,1,") and '"[3,4]"' in row
+
+
+def test_cli_defaults_match_the_reference():
+    # ref pfsp/lib/PFSP_lib.c:175-185: inst 14, lb 1, ub 1, m 25, M 50000, T 5000, D 1, C 1, ws 1, L 1, perc 50
+    from dist_gpu_accelerated_tree_search_amd.cli import _pfsp_parser
+
+    a = _pfsp_parser().parse_args([])
+    assert (a.inst, a.lb, a.ub, a.m, a.M, a.T, a.D, a.C, a.ws, a.L, a.perc) == \
+        (14, 1, 1, 25, 50000, 5000, 1, 1, 1, 1, 50)
+
+
+def test_dist_csv_uses_measured_load_balancing(tmp_path):
+    from dist_gpu_accelerated_tree_search_amd.utils import report
+
+    ws = [report.WorkerStats(tree=10, sol=1, gen_child=10, steals=3, success_steals=2, terminations=1,
+                             dist_load_bal=2, t_load_bal=0.25),
+          report.WorkerStats(tree=20, sol=0, gen_child=20, steals=0, success_steals=0, terminations=0,
+                             dist_load_bal=0, t_load_bal=0.0)]
+    path = tmp_path / "dist.csv"
+    report.write_dist_multi_gpu_csv(str(path), 14, 1, 1, 0, 1, 2, 1377, 25, 50000, 5000, 0.5, 30, 1, ws,
+                                    [w.dist_load_bal for w in ws], [w.t_load_bal for w in ws])
+    row = path.read_text().splitlines()[1]
+    assert '"[2,0]",' in row and '"[0.2500,0.0000]",' in row and '"[3,0]",' in row
