@@ -409,6 +409,7 @@ inline void bind_runner(py::module_& m, StagingFactory staging = {}, CpusOfDevic
           d["steals"] = r.steals;
           d["success_steals"] = r.success_steals;
           d["idle_rounds"] = r.idle_rounds;
+          d["early_rounds"] = r.early_rounds;
           ws_out.append(d);
         }
         py::dict out;

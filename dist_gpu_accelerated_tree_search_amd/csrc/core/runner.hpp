@@ -89,6 +89,7 @@ struct WorkerReport {
   unsigned long long rounds = 0, sent = 0, received = 0, transfers_in = 0, transfers_out = 0;
   unsigned long long device_transfers = 0, dropped_transfers = 0, watchdog_events = 0;
   unsigned long long steals = 0, success_steals = 0, idle_rounds = 0;  // ref nbSteals / nbSSteals / nbTermination
+  unsigned long long early_rounds = 0;  // rounds this worker called early (ran dry while a peer could donate)
   double t_run = 0, t_comm = 0, t_idle = 0, t_termination = 0;
   bool pinned = false;
 };
@@ -159,6 +160,9 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
                             rcap = per(cfg.recv_cap, cfg.steal_cap);
   bool done = false;
   int gbest = best;
+  std::vector<std::atomic<size_t>> live(W);
+  for (auto& x : live) x.store(0);
+  std::atomic<unsigned long long> request{0};
   double slice = cfg.slice_min;
   RoundBarrier bar(W);
   std::mutex stage_mu;
@@ -236,6 +240,12 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
     beat(w, Phase::Start);
     const std::vector<uint8_t>& init = initial[w];
     guarded([&] { e->begin(init.data(), init.size() / nb, best); });
+    // early rounds (as in dist_rounds.hpp): publish the live pool size after every
+    // replay; leave the slice when a dry worker asked for the next round
+    e->set_progress_hook([&, w](size_t pool) {
+      live[w].store(pool, std::memory_order_relaxed);
+      return cfg.work_sharing && request.load(std::memory_order_acquire) > rep[w].rounds;
+    });
     for (;;) {
       const auto t0 = now();
       beat(w, Phase::Run);
@@ -255,6 +265,18 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
         sizes[w] = e->size();
         bests[w] = e->best();
       });
+      live[w].store(sizes[w], std::memory_order_relaxed);
+      if (cfg.work_sharing && W > 1 && sizes[w] < needy[w]) {  // dry: call the round early if someone can donate
+        for (int x = 0; x < W; ++x)
+          if (x != w && live[x].load(std::memory_order_relaxed) >= donor[x]) {
+            unsigned long long cur = request.load();
+            const unsigned long long want = rep[w].rounds + 1;
+            while (cur < want && !request.compare_exchange_weak(cur, want)) {
+            }
+            ++rep[w].early_rounds;
+            break;
+          }
+      }
       beat(w, Phase::Barrier);
       TTS_RANGE("tts.round");
       bar.wait();
@@ -364,6 +386,7 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
       r.t_comm += secs(t1, now());
     }
     beat(w, Phase::Done);
+    e->set_progress_hook(nullptr);
     guarded([&] { r.st = e->stats(); });
   };
 

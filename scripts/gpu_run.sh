@@ -36,6 +36,10 @@ for step in "$@"; do
           -- python3 scripts/profile_workload.py "$wl" > "$out/trace_$wl.log" 2>&1 ) || { tail -20 "$out/trace_$wl.log"; exit 1; }
       python3 scripts/overlap.py "$out/trace_$wl" > "$out/overlap_$wl.txt"; rm -rf "$out/trace_$wl"
       grep -v "^W20\|^E20\|amdgpu.ids" "$out/trace_$wl.log" | tail -2; cat "$out/overlap_$wl.txt" ;;
+    py:*)  # py:<script.py>: any probe script, output to <out>/<script>.txt
+      sc="${step#py:}"; nm=$(basename "$sc" .py)
+      timeout -k 10 300 python -u "$sc" > "$out/$nm.txt" 2>&1 || { tail -20 "$out/$nm.txt"; exit 1; }
+      grep -v "amdgpu.ids" "$out/$nm.txt" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
         || { tail -20 "$out/smoke.log"; exit 1; }
