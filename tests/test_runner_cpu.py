@@ -125,3 +125,33 @@ def test_cpulist_parser():
     assert C.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
     assert C.parse_cpulist("") == []
     assert len(C.allowed_cpus()) >= 1
+
+
+def test_knuth_estimate_brackets_known_trees():
+    # unbiased random-probe estimate of the explored tree (csrc/core/estimate.hpp)
+    from dist_gpu_accelerated_tree_search_amd import PfspModel, QueensModel, ops
+
+    C = ops.cpu()
+    m = PfspModel(14, 0)
+    e = C.tree_estimate(m, m.best_known, 200000, 7, 6)  # deterministic for (probes, seed, threads)
+    assert 0.5 * 2573652 < e["tree"] < 2.0 * 2573652, e["tree"]
+    assert e["per_level"][0] == float(len(m.warmup(m.best_known, 2)[0]))  # level 1 is exact: the root's pushed children
+    q = C.tree_estimate(QueensModel(10), 0, 20000, 5, 2)
+    assert 0.7 * 35538 < q["tree"] < 1.3 * 35538, q["tree"]
+
+
+def test_pool_weight_progress_on_cpu_engine():
+    from dist_gpu_accelerated_tree_search_amd import PfspModel, ops
+    from dist_gpu_accelerated_tree_search_amd.search import progress_weights
+
+    m = PfspModel(14, 0)
+    w = progress_weights(m)
+    assert w[0] == 1.0 and abs(w[1] - 1 / 20) < 1e-15
+    e = ops.cpu().make_pfsp_cpu_engine(m.native, 0, 64, 1)
+    e.begin(m.root(), m.best_known)
+    assert e.pool_weight(w) == 1.0
+    e.run(max_launches=3)
+    mid = e.pool_weight(w)
+    assert 0.0 <= mid < 1.0
+    e.run()
+    assert e.pool_weight(w) == 0.0
