@@ -167,6 +167,36 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("device") = 0, py::arg("variant") = 0,
       "One production expand iteration over these parents with the debug output on: every child's bound "
       "(exact LB2 below best, else >= best). variant 0 prefix/suffix, 1 rounds, 2 dense, 3 wave.");
+  m.def(
+      "pfsp_expand_time",
+      [](int jobs, int machines, std::vector<int> p, int lb, U8 parents, int best, int device, int variant, int reps) {
+        const PfspInstance in = make_instance(jobs, machines, std::move(p));
+        const size_t nb = with_pfsp_bucket(jobs, [](auto nj) { return sizeof(PfspNode<decltype(nj)::value>); });
+        if (parents.ndim() != 2 || static_cast<size_t>(parents.shape(1)) != nb)
+          throw std::invalid_argument("parents must be a (n, node_bytes) uint8 array");
+        std::vector<double> t;
+        {
+          py::gil_scoped_release nogil;
+          (void)pfsp_expand_probe(in, lb, parents.data(), static_cast<size_t>(parents.shape(0)), best, device, variant,
+                                  reps, &t);
+        }
+        py::dict d;
+        d["ms_min"] = t[0];
+        d["ms_median"] = t[1];
+        d["clk_a"] = t[2];
+        d["clk_b1"] = t[3];
+        d["clk_b2"] = t[4];
+        d["clk_c"] = t[5];
+        d["chunks"] = t[6];
+        d["clk_block_max"] = t[7];
+        d["clk_block_mean"] = t[8];
+        d["grid"] = t[9];
+        return d;
+      },
+      py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("parents"), py::arg("best"),
+      py::arg("device") = 0, py::arg("variant") = 1, py::arg("reps") = 10,
+      "Time one expand iteration over this window (LB2): min/median ms over reps launches on the engine's grid, "
+      "and per-chunk shader clocks of phases A, B1, B2, B3+C from one instrumented launch.");
 
   m.def(
       "queens_labels",

@@ -598,6 +598,7 @@ class DeviceEngine final : public IEngine {
   // so the shadow can be edited again immediately).
   void upload_ctl() {
     TTS_HIP_CHECK(hipEventSynchronize(up_done_));
+    for (auto& sl : h_ctl_->slot) sl.qnext = 0;
     std::memcpy(h_up_, h_ctl_, sizeof(dev::PoolCtl));
     TTS_HIP_CHECK(hipMemcpyAsync(d_ctl_, h_up_, sizeof(dev::PoolCtl), hipMemcpyHostToDevice, stream_));
     TTS_HIP_CHECK(hipEventRecord(up_done_, stream_));

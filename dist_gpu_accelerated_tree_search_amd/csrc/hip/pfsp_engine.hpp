@@ -56,7 +56,43 @@ struct PfspTableImages {
   std::vector<uint16_t> ptab;  // [N][MS]
   std::vector<uint2> recs;     // [P][N]
   std::vector<uint2> pinfo;    // [P]
+  std::vector<uint4> recs4;    // [P][rs4]: recs padded with zero records (lb2_walk_pipe)
+  int rs4 = 0;
 };
+
+// Software-pipelined record loads in the LB2 walks (lb2_walk_pipe): on unless
+// TTS_LB2_PIPE=0 (A/B).
+inline int lb2_pipe_wanted() {
+  const char* f = std::getenv("TTS_LB2_PIPE");
+  return f ? (std::atoi(f) != 0) : 1;
+}
+
+// The LB2 kernel with two children per lane in packed u16 walks (LBK 5): every walk
+// value is at most the sum of all processing times, which must fit 16 bits, and job
+// sets must fit one word. On when it applies unless TTS_LB2_PK=0 (A/B).
+inline bool lb2_pk_ok(const PfspInstance& in) {
+  if (in.jobs > 64) return false;
+  long tot = 0;
+  for (int v : in.p) tot += v;
+  return tot < 65536;
+}
+inline bool lb2_pk_wanted(const PfspInstance& in) {
+  const char* f = std::getenv("TTS_LB2_PK");
+  return (f ? std::atoi(f) != 0 : true) && lb2_pk_ok(in);
+}
+
+// Dynamic chunk deal in the LB2 expand kernel: TTS_LB2_DYN=1 (A/B; measured slower
+// than the static deal of strided chunks: the queue atomic's return holds up the
+// chunk's first loads).
+inline int lb2_dyn_wanted() {
+  const char* f = std::getenv("TTS_LB2_DYN");
+  return f ? (std::atoi(f) != 0) : 0;
+}
+// Strided LB2 chunks (parents ch + i * nchunks): on unless TTS_LB2_STRIDE=0 (A/B).
+inline int lb2_stride_wanted() {
+  const char* f = std::getenv("TTS_LB2_STRIDE");
+  return f ? (std::atoi(f) != 0) : 1;
+}
 
 // Machine counts below the kernel's M are padded with trailing machines of zero
 // processing time: the makespan, every LB1 machine term and the fronts of the real
@@ -87,6 +123,23 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
       img.recs[static_cast<size_t>(q) * in.jobs + r] = rc;
     }
   }
+  {
+    const int ndouble = (in.jobs + 7) / 8;
+    img.rs4 = 4 * ndouble + 4;  // walks of ndouble x 8 records + one double group of prefetch
+    img.recs4.assign(static_cast<size_t>(PR) * img.rs4, make_uint4(0, 0, 0, 0));
+    for (int q = 0; q < PR; ++q)
+      for (int r = 0; r < in.jobs; ++r) {
+        const uint2 rc = img.recs[static_cast<size_t>(q) * in.jobs + r];
+        uint4& v = img.recs4[static_cast<size_t>(q) * img.rs4 + r / 2];
+        if (r & 1) {
+          v.z = rc.x;
+          v.w = rc.y;
+        } else {
+          v.x = rc.x;
+          v.y = rc.y;
+        }
+      }
+  }
   // expand kernel's pair table in the learned early-exit order (lb2_pair_order);
   // recs stay in the reference order (the bounds kernel keeps its exact partial
   // values) and pinfo points each slot at its pair's records
@@ -106,6 +159,10 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
   }
   a.jobs = in.jobs;
   a.npairs = PR;
+  a.rs4 = img.rs4;
+  a.lb2_pipe = lb2_pipe_wanted();
+  a.lb2_dyn = lb2_dyn_wanted();
+  a.lb2_stride = lb2_stride_wanted();
   for (int m = 0; m < M; ++m) {
     if (m < MR) {
       a.min_heads[m] = in.min_heads[m];
@@ -173,6 +230,7 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   a.ptab = upload_vec(img.ptab);
   a.recs = upload_vec(img.recs);
   a.pinfo = upload_vec(img.pinfo);
+  a.recs4 = upload_vec(img.recs4);
   // wave-uniform pair walks measured 2.6x slower on ta056 (active children per chunk
   // fill a fraction of a wave, profiles/r1/r1af): dense (pair, child) tasks by default
   a.lb2_wave = 0;
@@ -186,6 +244,7 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   eng->adopt(const_cast<uint16_t*>(a.ptab));
   eng->adopt(const_cast<uint2*>(a.recs));
   eng->adopt(const_cast<uint2*>(a.pinfo));
+  eng->adopt(const_cast<uint4*>(a.recs4));
   return eng;
 }
 
@@ -233,11 +292,16 @@ std::vector<int> pfsp_gpu_bounds_t(const PfspInstance& in, const void* parents, 
 // over `n` parents loaded as the window, with the kernel's debug output on. Returns
 // every child's bound in parent order (children k = depth..N-1): the exact LB2 when
 // it is below `best`, otherwise a value >= best (the kernel's prune decision).
-// variant: 0 prefix/suffix walks (default), 1 rounds of dense walks, 2 dense walks,
-// 3 wave-uniform walks.
+// variant: 0 prefix/suffix walks (kernel LBK 4), 1 rounds of dense walks, 2 dense
+// walks, 3 wave-uniform walks, 4 rounds of packed two-child walks (kernel LBK 5, the
+// default search path where lb2_pk_ok).
+// With `timing`: `reps` more launches without the debug output, each from the same
+// window (ring and control block restored), on the engine's grid (resident
+// workgroups), then one launch with the phase timers; timing = {min ms, median ms,
+// phase A, B1, B2, B3+C shader clocks per chunk, chunks}.
 template <int NJ, int M, int LBK>
 std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents, size_t n, int best, int device,
-                                     int variant) {
+                                     int variant, int reps = 0, std::vector<double>* timing = nullptr) {
   using Node = PfspNode<NJ>;
   using G = dev::PfspGeom<NJ, LBK, M>;
   if constexpr (LBK != 2) {
@@ -270,9 +334,10 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
     a.ptab = up(img.ptab);
     a.recs = up(img.recs);
     a.pinfo = up(img.pinfo);
+    a.recs4 = up(img.recs4);
     a.dbg_off = up(offsets);
     a.dbg_lb = up(out);
-    a.lb2_rounds = variant == 1;
+    a.lb2_rounds = variant == 1 || variant == 4;
     a.lb2_wave = variant == 3;
     size_t cap = 1;
     while (cap < n) cap *= 2;
@@ -293,14 +358,65 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
     pa.cap_mask = cap - 1;
     pa.max_parents = static_cast<int>(nchunks * G::BP);
     pa.max_chunks = static_cast<int>(nchunks);
-    const dim3 grid(static_cast<unsigned>(std::min<size_t>(nchunks, 1024)));
-    if (variant == 0)
-      hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, 4>), grid, dim3(dev::kBlock), 0, 0, a, 0);
-    else
-      hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), grid, dim3(dev::kBlock), 0, 0, a, 0);
-    TTS_HIP_CHECK(hipGetLastError());
+    if (variant == 4 && !lb2_pk_ok(in)) throw std::invalid_argument("expand probe: packed walks do not apply");
+    auto launch = [&](const dim3& grid) {
+      if (variant == 0)
+        hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, 4>), grid, dim3(dev::kBlock), 0, 0, a, 0);
+      else if (variant == 4)
+        hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, 5>), grid, dim3(dev::kBlock), 0, 0, a, 0);
+      else
+        hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), grid, dim3(dev::kBlock), 0, 0, a, 0);
+      TTS_HIP_CHECK(hipGetLastError());
+    };
+    launch(dim3(static_cast<unsigned>(std::min<size_t>(nchunks, 1024))));
     TTS_HIP_CHECK(hipDeviceSynchronize());
     TTS_HIP_CHECK(hipMemcpy(out.data(), a.dbg_lb, nb * sizeof(int), hipMemcpyDeviceToHost));
+    if (timing) {
+      int bpc = 0, cus = 0;
+      if (variant == 0)
+        TTS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::pfsp_expand_kernel<NJ, M, 4>,
+                                                                   dev::kBlock, 0));
+      else if (variant == 4)
+        TTS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::pfsp_expand_kernel<NJ, M, 5>,
+                                                                   dev::kBlock, 0));
+      else
+        TTS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::pfsp_expand_kernel<NJ, M, LBK>,
+                                                                   dev::kBlock, 0));
+      TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+      const dim3 grid(static_cast<unsigned>(std::min<size_t>(nchunks, static_cast<size_t>(std::max(1, bpc * cus)))));
+      a.dbg_lb = nullptr;
+      auto restore = [&] {
+        TTS_HIP_CHECK(hipMemcpy(pa.ring, ph, n * sizeof(Node), hipMemcpyHostToDevice));
+        TTS_HIP_CHECK(hipMemcpy(pa.ctl, &h, sizeof(h), hipMemcpyHostToDevice));
+      };
+      hipEvent_t e0, e1;
+      TTS_HIP_CHECK(hipEventCreate(&e0));
+      TTS_HIP_CHECK(hipEventCreate(&e1));
+      std::vector<double> ms;
+      for (int r = 0; r < std::max(1, reps); ++r) {
+        restore();
+        TTS_HIP_CHECK(hipEventRecord(e0, 0));
+        launch(grid);
+        TTS_HIP_CHECK(hipEventRecord(e1, 0));
+        TTS_HIP_CHECK(hipEventSynchronize(e1));
+        float t = 0;
+        TTS_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+        ms.push_back(t);
+      }
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      std::sort(ms.begin(), ms.end());
+      restore();
+      a.dbg_time = static_cast<unsigned long long*>(dalloc(8 * sizeof(unsigned long long)));
+      launch(grid);
+      TTS_HIP_CHECK(hipDeviceSynchronize());
+      unsigned long long tm[8] = {};
+      TTS_HIP_CHECK(hipMemcpy(tm, a.dbg_time, sizeof(tm), hipMemcpyDeviceToHost));
+      const double nc = static_cast<double>(std::max<unsigned long long>(1, tm[4]));
+      *timing = {ms.front(), ms[ms.size() / 2], tm[0] / nc, tm[1] / nc, tm[2] / nc, tm[3] / nc, nc,
+                 static_cast<double>(tm[5]), static_cast<double>(tm[6]) / std::max<unsigned long long>(1, tm[7]),
+                 static_cast<double>(grid.x)};
+    }
     for (void* d : owned) (void)hipFree(d);
     return out;
   }
@@ -320,14 +436,14 @@ decltype(auto) with_machine_bucket(int machines, F&& f) {
 std::unique_ptr<IEngine> make_pfsp_engine(const PfspInstance& in, int lb, const EngineConfig& cfg);
 std::vector<int> pfsp_gpu_bounds(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device);
 std::vector<int> pfsp_expand_probe(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device,
-                                   int variant);
+                                   int variant, int reps = 0, std::vector<double>* timing = nullptr);
 
 #define TTS_PFSP_DECLARE_BUCKET(NJ)                                                                   \
   std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg); \
   std::vector<int> pfsp_gpu_bounds_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
                                           int device);                                                \
   std::vector<int> pfsp_expand_probe_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
-                                            int device, int variant);
+                                            int device, int variant, int reps, std::vector<double>* timing);
 TTS_PFSP_DECLARE_BUCKET(20)
 TTS_PFSP_DECLARE_BUCKET(50)
 TTS_PFSP_DECLARE_BUCKET(100)
@@ -344,6 +460,8 @@ TTS_PFSP_DECLARE_BUCKET(500)
       if constexpr (NJ == 50)                                                                        \
         if (lb2_pack_wanted(in)) return make_pfsp_engine_t<NJ, M, 3>(in, cfg);                       \
       if (lb2_ps_wanted()) return make_pfsp_engine_t<NJ, M, 4>(in, cfg);                             \
+      if constexpr (NJ <= 64)                                                                        \
+        if (M >= 10 && lb2_pk_wanted(in)) return make_pfsp_engine_t<NJ, M, 5>(in, cfg);               \
       return make_pfsp_engine_t<NJ, M, 2>(in, cfg);                                                  \
     });                                                                                              \
   }                                                                                                  \
@@ -356,11 +474,11 @@ TTS_PFSP_DECLARE_BUCKET(500)
     });                                                                                              \
   }                                                                                                  \
   std::vector<int> pfsp_expand_probe_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
-                                            int device, int variant) {                               \
+                                            int device, int variant, int reps, std::vector<double>* timing) { \
     if (lb != 2) throw std::invalid_argument("expand probe: LB2 only");                             \
     return with_machine_bucket(in.machines, [&](auto mm) {                                           \
       constexpr int M = decltype(mm)::value;                                                         \
-      return pfsp_expand_probe_t<NJ, M, 2>(in, parents, n, best, device, variant);                  \
+      return pfsp_expand_probe_t<NJ, M, 2>(in, parents, n, best, device, variant, reps, timing);    \
     });                                                                                              \
   }
 

@@ -24,13 +24,13 @@ std::vector<int> pfsp_gpu_bounds(const PfspInstance& in, int lb, const void* par
 }
 
 std::vector<int> pfsp_expand_probe(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device,
-                                   int variant) {
+                                   int variant, int reps, std::vector<double>* timing) {
   switch (pfsp_bucket(in.jobs)) {
-    case 20: return pfsp_expand_probe_nj20(in, lb, parents, n, best, device, variant);
-    case 50: return pfsp_expand_probe_nj50(in, lb, parents, n, best, device, variant);
-    case 100: return pfsp_expand_probe_nj100(in, lb, parents, n, best, device, variant);
-    case 200: return pfsp_expand_probe_nj200(in, lb, parents, n, best, device, variant);
-    default: return pfsp_expand_probe_nj500(in, lb, parents, n, best, device, variant);
+    case 20: return pfsp_expand_probe_nj20(in, lb, parents, n, best, device, variant, reps, timing);
+    case 50: return pfsp_expand_probe_nj50(in, lb, parents, n, best, device, variant, reps, timing);
+    case 100: return pfsp_expand_probe_nj100(in, lb, parents, n, best, device, variant, reps, timing);
+    case 200: return pfsp_expand_probe_nj200(in, lb, parents, n, best, device, variant, reps, timing);
+    default: return pfsp_expand_probe_nj500(in, lb, parents, n, best, device, variant, reps, timing);
   }
 }
 

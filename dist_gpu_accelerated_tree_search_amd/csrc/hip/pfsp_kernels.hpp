@@ -99,6 +99,25 @@ struct PfspArgs {
   // parent i at dbg_lb[dbg_off[i] + (k - depth)] (exact LB2 below best, else >= best)
   int* dbg_lb;
   const int* dbg_off;
+  // LB2 records again, padded per pair to rs4 16-B vectors (two records each, zero
+  // records after the last job: a zero record is a no-op step, see lb2_walk_pipe) for
+  // the software-pipelined walk; lb2_pipe selects it (default on)
+  const uint4* recs4;
+  int rs4;
+  int lb2_pipe;
+  // LB2 chunks dealt dynamically (a per-iteration counter in the control slot) instead
+  // of chunk = blockIdx.x + k * gridDim.x: active children per chunk vary ~4x, and a
+  // static deal leaves the iteration waiting on its unluckiest workgroup
+  int lb2_dyn;
+  // LB2 chunk ch takes window parents ch, ch + nchunks, ch + 2 nchunks, ... instead of
+  // BP consecutive ones: consecutive pool nodes are siblings with similar work, so
+  // consecutive chunks ranged from 0 to ~4x the mean active children and the slowest
+  // workgroup took twice the mean (ta056 windows, scripts/lb2_kernel_bench.py)
+  int lb2_stride;
+  // phase timers of the LB2 expand kernel (probe only): shader clocks summed over the
+  // workgroups for phases A, B1, B2, B3+C, the chunk count, the largest and the summed
+  // per-workgroup totals, and the workgroups that had a chunk
+  unsigned long long* dbg_time;
 };
 
 template <int NJ, int M, int LBK>
@@ -181,6 +200,76 @@ __device__ inline int pfsp_phase_a(const PfspArgs<NJ, M>& a, Smem& sm, int nvali
   if (tid < nvalid) {
     sm.off[tid] = off;
     for (int j = 0; j < nchild; ++j) sm.map[off + j] = static_cast<typename G::map_t>(tid);
+  }
+  __syncthreads();
+  return total;
+}
+
+// Phase A of the LB2 expand kernel, machine-parallel. The prefix replay
+// f[i][m] = max(f[i-1][m], f[i][m-1]) + p[job_i][m] is a 2-D recurrence: lane m of a
+// parent's M-lane group computes column m one step behind lane m - 1 (anti-diagonal
+// wavefront, the left neighbour's value comes in by a lane shuffle), so a parent at
+// depth d costs d + M - 1 steps instead of d * M dependent steps on one lane (the
+// serial replay was ~18 % of the kernel's clocks on ta056 windows, 8 lanes of 256
+// busy). Several parents per wave (64 / M), all waves.
+template <int NJ, int M, class Smem, class Src>
+__device__ inline int pfsp_phase_a_wf(const PfspArgs<NJ, M>& a, Smem& sm, int nvalid, Src src) {
+  using G = PfspGeom<NJ, 2, M>;
+  using Node = PfspNode<NJ>;
+  constexpr int VPN = sizeof(Node) / 16;
+  constexpr int PW = kWave / M;                 // parent groups per wave
+  constexpr int PB = PW * (kBlock / kWave);     // parents per pass
+  static_assert(PW >= 1, "one parent group per wave at least");
+  const int tid = threadIdx.x;
+  for (int v = tid; v < nvalid * VPN; v += kBlock) {
+    const int i = v / VPN, w = v - i * VPN;
+    reinterpret_cast<uint4*>(&sm.node[i])[w] = reinterpret_cast<const uint4*>(src(i))[w];
+  }
+  for (int i = tid; i < nvalid * G::NW; i += kBlock) (&sm.pmask[0][0])[i] = 0;
+  __syncthreads();
+  const int lane = tid & (kWave - 1), wave = tid >> 6;
+  const int gl = lane / M, m = lane - gl * M;
+  for (int base = 0; base < nvalid; base += PB) {
+    const int p = base + wave * PW + gl;
+    const bool own = gl < PW && p < nvalid;
+    const int d = own ? static_cast<int>(sm.node[own ? p : 0].depth) : 0;
+    int steps = own ? d + m : 0;  // lane m's last step is d - 1 + m
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o, kWave));
+    int f = 0, r = own ? a.sum_all[m] : 0;
+    for (int s = 0; s < steps; ++s) {
+      const int left = __shfl_up(f, 1, kWave);
+      const int i = s - m;
+      if (own && i >= 0 && i < d) {
+        const int pv = sm.ptab[sm.node[p].prmu[i]][m];
+        f = max(f, m > 0 ? left : 0) + pv;
+        r -= pv;
+      }
+    }
+    if (own) {
+      if (d == 0) f = a.min_heads[m];
+      sm.fr[p][m] = static_cast<uint32_t>(f) | (static_cast<uint32_t>(r) << 16);
+      for (int i = m; i < d; i += M) {
+        const int job = sm.node[p].prmu[i];
+        atomicOr(&sm.pmask[p][job >> 6], 1ull << (job & 63));
+      }
+    }
+  }
+  const int nchild = tid < nvalid ? a.jobs - static_cast<int>(sm.node[tid].depth) : 0;
+  int total = 0;
+  const int off = block_exclusive_scan(nchild, sm.scan, &total);
+  if (tid < nvalid) sm.off[tid] = off;
+  __syncthreads();
+  for (int c = tid; c < total; c += kBlock) {
+    int lo = 0, hi = nvalid - 1;  // last parent with off <= c
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sm.off[mid] <= c)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    sm.map[c] = static_cast<typename G::map_t>(lo);
   }
   __syncthreads();
   return total;
@@ -380,14 +469,16 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 
-template <int NJ, int M, bool PACK, bool PS>
+template <int NJ, int M, bool PACK, bool PS, bool PK = false>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 
 // Occupancy: the LB1 kernels are latency-bound (profiles/r1/r1o), so the register
 // budget is capped for more resident waves (6 per SIMD for M <= 10: 80 VGPRs, no
-// spills); LB2 is bounded by its LDS footprint instead.
+// spills); LB2 is bounded by its LDS footprint instead (4 workgroups per CU for
+// 50 x 20), and the packed-walk kernel (LBK 5) is held to the 128 VGPRs of 4 waves
+// per SIMD (its unrolled walk would otherwise take 130).
 template <int NJ, int M, int LBK>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK == 5 ? 4 : LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
 void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
     pfsp_expand_lb2<NJ, M, false, false>(a, t);
@@ -395,6 +486,10 @@ void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
     pfsp_expand_lb2<NJ, M, true, false>(a, t);  // records packed in LDS
   else if constexpr (LBK == 4)
     pfsp_expand_lb2<NJ, M, false, true>(a, t);  // prefix/suffix walks per (parent, pair)
+  else if constexpr (LBK == 5 && NJ <= 64)
+    pfsp_expand_lb2<NJ, M, false, false, true>(a, t);  // two children per lane, packed u16 walks
+  else if constexpr (LBK == 5)
+    pfsp_expand_lb2<NJ, M, false, false>(a, t);  // (job sets of one word only)
   else if constexpr (sizeof(PfspNode<NJ>) == 32)
     pfsp_expand_lb1_small<NJ, M>(a, t);
   else
@@ -444,6 +539,7 @@ struct PfspSmemLB2 {
   uint8_t palive[G::BP];                  // parent still has an active child below best
   uint8_t plist[G::BP];                   // ... compacted
   int npl;
+  int qch;                                // next chunk (dynamic deal)
   u64 bits[G::NWORDS + kBlock / kWave];
   int wpre[kBlock];
   int scan[kBlock / kWave];
@@ -712,7 +808,94 @@ __device__ inline void lb2_johnson_walk(const S& sm, const uint2* recs, int qs, 
   }
 }
 
-template <int NJ, int M, bool PACK, bool PS>
+// Johnson step on one record {x = job | p0 << 16, y = p1 | lag << 16}.
+template <int NW>
+__device__ inline void lb2_step(uint32_t x, uint32_t y, const u64 (&msk)[NW], int& t0, int& t1) {
+  const int n0 = t0 + static_cast<int>(x >> 16);
+  const int n1 = max(t1, n0 + static_cast<int>(y >> 16)) + static_cast<int>(y & 0xffff);
+  const bool sched = job_in<NW>(msk, static_cast<int>(x & 0xffff));
+  t0 = sched ? t0 : n0;
+  t1 = sched ? t1 : n1;
+}
+
+// The Johnson walk with its record loads software-pipelined: the walk runs in
+// double groups of 8 records (four 16-B loads); group A's records for the next
+// double group are requested right after A is consumed, B's after B, so each load
+// has a whole group of steps (plus the other waves' issue) to land instead of
+// stalling the step that needs it (the plain loop waits on every load: L1/L2
+// latency per four steps). The table is padded per pair with zero records up to one
+// double group past the walk; a zero record is a no-op step (n0 = t0 and, as a
+// front on the later machine never trails the earlier one, n1 = max(t1, t0) = t1).
+template <int NW>
+__device__ inline void lb2_walk_pipe(const uint4* rq, int ndouble, const u64 (&msk)[NW], int& t0, int& t1) {
+  uint4 a0 = rq[0], a1 = rq[1], b0 = rq[2], b1 = rq[3];
+  for (int g = 0; g < ndouble; ++g) {
+    lb2_step<NW>(a0.x, a0.y, msk, t0, t1);
+    lb2_step<NW>(a0.z, a0.w, msk, t0, t1);
+    lb2_step<NW>(a1.x, a1.y, msk, t0, t1);
+    lb2_step<NW>(a1.z, a1.w, msk, t0, t1);
+    a0 = rq[4 * g + 4];
+    a1 = rq[4 * g + 5];
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch here (the scheduler sinks it to its use)
+    lb2_step<NW>(b0.x, b0.y, msk, t0, t1);
+    lb2_step<NW>(b0.z, b0.w, msk, t0, t1);
+    lb2_step<NW>(b1.x, b1.y, msk, t0, t1);
+    lb2_step<NW>(b1.z, b1.w, msk, t0, t1);
+    b0 = rq[4 * g + 6];
+    b1 = rq[4 * g + 7];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Two children per lane (kernel LBK 5): both walk the same machine pair, so one
+// record load serves two Johnson steps and the max-plus arithmetic runs on packed u16
+// halves (v_pk_add_u16 / v_pk_max_u16, the record fields broadcast by op_sel); each
+// half skips the jobs of its own child's scheduled set (bit field insert on a
+// per-half keep mask). Exact as long as every value of the walk fits 16 bits: a walk
+// value is a path length through the p matrix, at most the sum of all processing
+// times (host check lb2_pk_ok: < 65536).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ inline uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+__device__ inline void lb2_step2(uint32_t x, uint32_t y, u64 ma, u64 mb, uint32_t& t0, uint32_t& t1) {
+  const u16x2 p0 = static_cast<u16x2>(static_cast<unsigned short>(x >> 16));
+  const u16x2 lag = static_cast<u16x2>(static_cast<unsigned short>(y >> 16));
+  const u16x2 p1 = static_cast<u16x2>(static_cast<unsigned short>(y & 0xffff));
+  const u16x2 n0 = as_u16x2(t0) + p0;
+  const u16x2 n1 = __builtin_elementwise_max(as_u16x2(t1), n0 + lag) + p1;
+  const uint32_t job = x & 63u;
+  // all ones where the half's child skips the job: v_lshrrev_b64 + v_bfe_i32 per child
+  // (spelled with the intrinsics: the plain (m >> job) & 1 becomes a mask-and-compare
+  // sequence twice as long), halves merged by one v_perm_b32
+  const int ka = __builtin_amdgcn_sbfe(static_cast<int>(static_cast<uint32_t>(ma >> job)), 0, 1);
+  const int kb = __builtin_amdgcn_sbfe(static_cast<int>(static_cast<uint32_t>(mb >> job)), 0, 1);
+  const uint32_t keep = __builtin_amdgcn_perm(static_cast<uint32_t>(kb), static_cast<uint32_t>(ka), 0x05040100u);
+  t0 = (t0 & keep) | (as_u32(n0) & ~keep);
+  t1 = (t1 & keep) | (as_u32(n1) & ~keep);
+}
+
+__device__ inline void lb2_walk_pipe2(const uint4* rq, int ndouble, u64 ma, u64 mb, uint32_t& t0, uint32_t& t1) {
+  uint4 a0 = rq[0], a1 = rq[1], b0 = rq[2], b1 = rq[3];
+  for (int g = 0; g < ndouble; ++g) {
+    lb2_step2(a0.x, a0.y, ma, mb, t0, t1);
+    lb2_step2(a0.z, a0.w, ma, mb, t0, t1);
+    lb2_step2(a1.x, a1.y, ma, mb, t0, t1);
+    lb2_step2(a1.z, a1.w, ma, mb, t0, t1);
+    a0 = rq[4 * g + 4];
+    a1 = rq[4 * g + 5];
+    __builtin_amdgcn_sched_barrier(0);
+    lb2_step2(b0.x, b0.y, ma, mb, t0, t1);
+    lb2_step2(b0.z, b0.w, ma, mb, t0, t1);
+    lb2_step2(b1.x, b1.y, ma, mb, t0, t1);
+    lb2_step2(b1.z, b1.w, ma, mb, t0, t1);
+    b0 = rq[4 * g + 6];
+    b1 = rq[4 * g + 7];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int NJ, int M, bool PACK, bool PS, bool PK>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   using G = PfspGeom<NJ, 2, M>;
   using C = PfspConsts<M>;
@@ -724,6 +907,8 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   __shared__ S sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
+  // the next iteration's chunk queue (its slot is not read by this iteration)
+  if (a.lb2_dyn && blockIdx.x == 0 && tid == 0) pa.ctl->slot[(t + 1) % 3].qnext = 0;
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
   if (v.B == 0 || v.overflow) return;
   const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -746,12 +931,40 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   }
   const uint2* recs = S::kRecsInLds ? sm.recs : a.recs;
   const int N = a.jobs;
-  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
-    const u64 first = static_cast<u64>(ch) * G::BP;
-    const int nvalid = static_cast<int>(min(static_cast<u64>(G::BP), v.B - first));
-    const int total = pfsp_phase_a<NJ, M, 2>(a, sm, nvalid, [&](int i) -> const Node* {
-      return pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, first + i, sm.pool);
-    });
+  const bool pipe = !PACK && !S::kRecsInLds && a.lb2_pipe;
+  const int ndouble = (N + 7) >> 3;
+  unsigned long long tm[4] = {0, 0, 0, 0}, tc = 0;
+  const bool timed = a.dbg_time != nullptr;
+  const bool dyn = a.lb2_dyn != 0;
+  const bool stride = a.lb2_stride != 0;
+  int* const qctr = &pa.ctl->slot[t % 3].qnext;
+  int ch = blockIdx.x;
+  if (dyn) {
+    if (tid == 0) sm.qch = atomicAdd(qctr, 1);
+    __syncthreads();
+    ch = sm.qch;
+  }
+  int nchunks_done = 0;
+  while (ch < v.nchunks) {
+    int qn = 0;
+    if (dyn && tid == 0) qn = atomicAdd(qctr, 1);  // next chunk, requested a chunk ahead
+    ++nchunks_done;
+    if (timed) tc = clock64();
+    // window parents of this chunk: ch + i * nchunks (strided) or ch * BP + i
+    const u64 first = stride ? static_cast<u64>(ch) : static_cast<u64>(ch) * G::BP;
+    const u64 step = stride ? static_cast<u64>(v.nchunks) : 1ull;
+    const int nvalid = stride ? static_cast<int>((v.B - first + step - 1) / step)
+                              : static_cast<int>(min(static_cast<u64>(G::BP), v.B - first));
+    auto gidx = [&](int i) -> u64 { return first + static_cast<u64>(i) * step; };
+    auto src = [&](int i) -> const Node* {
+      return pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gidx(i), sm.pool);
+    };
+    const int total = pfsp_phase_a_wf<NJ, M>(a, sm, nvalid, src);
+    if (timed) {
+      const unsigned long long c = clock64();
+      tm[0] += c - tc;
+      tc = c;
+    }
     // ---- B1: child fronts, LB1 filter, leaves, active list ----
     int my_leaves = 0, nact = 0;
     for (int cb = 0; cb < total; cb += kBlock) {
@@ -777,7 +990,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
           tt = sv + pr[m];
           f[m] = tt;
         }
-        const bool keep = split_keep(v, first + p, k);
+        const bool keep = split_keep(v, gidx(p), k);
         if (d + 1 == N) {
           // a leaf's LB2 is its makespan bound max_m(front + tail) == LB1
           my_leaves += keep;
@@ -786,7 +999,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
           active = (keep && lb1 < best) ? 1 : 0;
         }
         lb1c = lb1;
-        if (a.dbg_lb && !active) a.dbg_lb[a.dbg_off[first + p] + (k - d)] = lb1;
+        if (a.dbg_lb && !active) a.dbg_lb[a.dbg_off[gidx(p)] + (k - d)] = lb1;
       }
       int cnt = 0;
       const int slot = nact + block_exclusive_scan(active, sm.scan, &cnt);
@@ -807,6 +1020,11 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       nact += cnt;
     }
     __syncthreads();
+    if (timed) {
+      const unsigned long long c = clock64();
+      tm[1] += c - tc;
+      tc = c;
+    }
     // ---- B2: (pair, child) Johnson walks, pair-major ----
     if constexpr (PS) {
       if (nact > 0) lb2_ps_walks<NJ, M, PACK>(a, sm, nvalid, nact, best);
@@ -824,6 +1042,37 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       int na = nact, q0 = 0, R = 8;
       while (q0 < P && na > 0) {
         const int nq = min(P - q0, R);
+        if constexpr (PK) {
+          // tasks (pair, child pair): children alist[2k], alist[2k + 1] share a lane
+          static_assert(G::NW == 1, "packed walks: job sets of one word");
+          const int nk = (na + 1) >> 1;
+          int qq = tid / nk, kk = tid - (tid / nk) * nk;
+          const int dq = kBlock / nk, dk = kBlock - dq * nk;
+          while (qq < nq) {
+            const int ca = sm.alist[2 * kk];
+            const int cb = 2 * kk + 1 < na ? sm.alist[2 * kk + 1] : -1;
+            const bool la = sm.lbv[ca] < best, lbb = cb >= 0 && sm.lbv[cb] < best;
+            if (la || lbb) {
+              const uint2 pi = sm.pinfo[q0 + qq];
+              const int m0 = pi.x & 0xff, m1 = (pi.x >> 8) & 0xff;
+              const int cbb = cb >= 0 ? cb : ca;
+              uint32_t t0 = static_cast<uint32_t>(sm.cf[m0][ca]) | (static_cast<uint32_t>(sm.cf[m0][cbb]) << 16);
+              uint32_t t1 = static_cast<uint32_t>(sm.cf[m1][ca]) | (static_cast<uint32_t>(sm.cf[m1][cbb]) << 16);
+              const u64 ma = sm.cm[ca][0], mb = cb >= 0 ? sm.cm[cbb][0] : ~0ull;
+              lb2_walk_pipe2(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, ma, mb, t0, t1);
+              const int tl0 = static_cast<int>(pi.y & 0xffff), tl1 = static_cast<int>(pi.y >> 16);
+              if (la)
+                atomicMax(&sm.lbv[ca], max(static_cast<int>(t1 & 0xffff) + tl1, static_cast<int>(t0 & 0xffff) + tl0));
+              if (lbb) atomicMax(&sm.lbv[cb], max(static_cast<int>(t1 >> 16) + tl1, static_cast<int>(t0 >> 16) + tl0));
+            }
+            kk += dk;
+            qq += dq;
+            if (kk >= nk) {
+              kk -= nk;
+              ++qq;
+            }
+          }
+        } else {
         int qq = tid / na, ii = tid - (tid / na) * na;
         const int dq = kBlock / na, di = kBlock - dq * na;
         while (qq < nq) {
@@ -839,7 +1088,10 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
             u64 msk[G::NW];
 #pragma unroll
             for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
-            lb2_johnson_walk<NJ, M, PACK>(sm, recs, q0 + qq, pi, N, msk, t0, t1, uref);
+            if (pipe && uref < 0)
+              lb2_walk_pipe<G::NW>(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, msk, t0, t1);
+            else
+              lb2_johnson_walk<NJ, M, PACK>(sm, recs, q0 + qq, pi, N, msk, t0, t1, uref);
             atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
           }
           ii += di;
@@ -848,6 +1100,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
             ii -= na;
             ++qq;
           }
+        }
         }
         q0 += nq;
         R *= 2;
@@ -897,6 +1150,11 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       }
     }
     __syncthreads();
+    if (timed) {
+      const unsigned long long c = clock64();
+      tm[2] += c - tc;
+      tc = c;
+    }
     // ---- B3: survivor bitmap ----
     for (int cb = 0; cb < total; cb += kBlock) {
       const int c = cb + tid;
@@ -906,7 +1164,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         survive = s >= 0 && sm.lbv[s] < best;
         if (a.dbg_lb && s >= 0) {
           const int p = sm.map[c];
-          a.dbg_lb[a.dbg_off[first + p] + (c - sm.off[p])] = sm.lbv[s];
+          a.dbg_lb[a.dbg_off[gidx(p)] + (c - sm.off[p])] = sm.lbv[s];
         }
       }
       const u64 bal = __ballot(survive);
@@ -944,6 +1202,23 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       for (int q = 0; q < VPN; ++q) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
     }
     __syncthreads();
+    if (timed) tm[3] += clock64() - tc;
+    if (dyn) {
+      if (tid == 0) sm.qch = qn;
+      __syncthreads();
+      ch = sm.qch;
+    } else {
+      ch += gridDim.x;
+    }
+  }
+  if (timed && tid == 0) {
+    const unsigned long long tot = tm[0] + tm[1] + tm[2] + tm[3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) atomicAdd(&a.dbg_time[i], tm[i]);
+    atomicAdd(&a.dbg_time[4], static_cast<unsigned long long>(nchunks_done));
+    atomicMax(&a.dbg_time[5], tot);
+    atomicAdd(&a.dbg_time[6], tot);
+    if (nchunks_done) atomicAdd(&a.dbg_time[7], 1ull);
   }
 }
 
