@@ -191,6 +191,10 @@ PYBIND11_MODULE(_tts_hip, m) {
         d["clk_block_max"] = t[7];
         d["clk_block_mean"] = t[8];
         d["grid"] = t[9];
+        const size_t nblk = (t.size() - 10) / 3;
+        py::array_t<double> tl({static_cast<py::ssize_t>(nblk), static_cast<py::ssize_t>(3)});
+        std::memcpy(tl.mutable_data(), t.data() + 10, nblk * 3 * sizeof(double));
+        d["timeline_us"] = tl;
         return d;
       },
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("parents"), py::arg("best"),

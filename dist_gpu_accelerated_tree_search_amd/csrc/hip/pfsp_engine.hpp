@@ -412,10 +412,25 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
       TTS_HIP_CHECK(hipDeviceSynchronize());
       unsigned long long tm[8] = {};
       TTS_HIP_CHECK(hipMemcpy(tm, a.dbg_time, sizeof(tm), hipMemcpyDeviceToHost));
+      // workgroup timeline, from its own launch (no phase timers)
+      restore();
+      a.dbg_time = nullptr;
+      a.dbg_blk = static_cast<unsigned long long*>(dalloc(3 * grid.x * sizeof(unsigned long long)));
+      launch(grid);
+      TTS_HIP_CHECK(hipDeviceSynchronize());
+      std::vector<unsigned long long> blk(3 * grid.x);
+      TTS_HIP_CHECK(hipMemcpy(blk.data(), a.dbg_blk, blk.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      a.dbg_blk = nullptr;
+      int rate_khz = 0;
+      TTS_HIP_CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device));
+      unsigned long long t0 = ~0ull;
+      for (size_t i = 0; i < grid.x; ++i) t0 = std::min(t0, blk[3 * i]);
       const double nc = static_cast<double>(std::max<unsigned long long>(1, tm[4]));
       *timing = {ms.front(), ms[ms.size() / 2], tm[0] / nc, tm[1] / nc, tm[2] / nc, tm[3] / nc, nc,
                  static_cast<double>(tm[5]), static_cast<double>(tm[6]) / std::max<unsigned long long>(1, tm[7]),
                  static_cast<double>(grid.x)};
+      const double us = 1e3 / std::max(1, rate_khz);
+      for (unsigned long long x : blk) timing->push_back(static_cast<double>(x - t0) * us);
     }
     for (void* d : owned) (void)hipFree(d);
     return out;

@@ -118,6 +118,9 @@ struct PfspArgs {
   // workgroups for phases A, B1, B2, B3+C, the chunk count, the largest and the summed
   // per-workgroup totals, and the workgroups that had a chunk
   unsigned long long* dbg_time;
+  // per-workgroup timeline (probe only): wall clock (s_memrealtime) at entry, after
+  // the iteration prologue, and at exit, 3 values per workgroup
+  unsigned long long* dbg_blk;
 };
 
 template <int NJ, int M, int LBK>
@@ -208,7 +211,7 @@ __device__ inline int pfsp_phase_a(const PfspArgs<NJ, M>& a, Smem& sm, int nvali
 // Phase A of the LB2 expand kernel, machine-parallel. The prefix replay
 // f[i][m] = max(f[i-1][m], f[i][m-1]) + p[job_i][m] is a 2-D recurrence: lane m of a
 // parent's M-lane group computes column m one step behind lane m - 1 (anti-diagonal
-// wavefront, the left neighbour's value comes in by a lane shuffle), so a parent at
+// wavefront, the left neighbour's value comes in by a DPP lane shift), so a parent at
 // depth d costs d + M - 1 steps instead of d * M dependent steps on one lane (the
 // serial replay was ~18 % of the kernel's clocks on ta056 windows, 8 lanes of 256
 // busy). Several parents per wave (64 / M), all waves.
@@ -237,13 +240,25 @@ __device__ inline int pfsp_phase_a_wf(const PfspArgs<NJ, M>& a, Smem& sm, int nv
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o, kWave));
     int f = 0, r = own ? a.sum_all[m] : 0;
-    for (int s = 0; s < steps; ++s) {
-      const int left = __shfl_up(f, 1, kWave);
-      const int i = s - m;
-      if (own && i >= 0 && i < d) {
-        const int pv = sm.ptab[sm.node[p].prmu[i]][m];
-        f = max(f, m > 0 ? left : 0) + pv;
-        r -= pv;
+    for (int s0 = 0; s0 < steps; s0 += 8) {
+      // the next 8 p values of this lane's column, read together (two dependent LDS
+      // reads each: job, then p), then 8 wavefront steps
+      int pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = s0 + u - m;
+        pv[u] = (own && i >= 0 && i < d) ? static_cast<int>(sm.ptab[sm.node[p].prmu[i]][m]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        // left neighbour's column value by DPP wave_shr:1 (a VALU move; a shuffle
+        // through the LDS crossbar would put its latency on every step)
+        const int left = __builtin_amdgcn_update_dpp(0, f, 0x138, 0xf, 0xf, false);
+        const int i = s0 + u - m;
+        if (own && i >= 0 && i < d) {
+          f = max(f, m > 0 ? left : 0) + pv[u];
+          r -= pv[u];
+        }
       }
     }
     if (own) {
@@ -907,6 +922,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   __shared__ S sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
+  const unsigned long long t_entry = a.dbg_blk ? wall_clock64() : 0;
   // the next iteration's chunk queue (its slot is not read by this iteration)
   if (a.lb2_dyn && blockIdx.x == 0 && tid == 0) pa.ctl->slot[(t + 1) % 3].qnext = 0;
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
@@ -945,6 +961,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     ch = sm.qch;
   }
   int nchunks_done = 0;
+  const unsigned long long t_pro = a.dbg_blk ? wall_clock64() : 0;
   while (ch < v.nchunks) {
     int qn = 0;
     if (dyn && tid == 0) qn = atomicAdd(qctr, 1);  // next chunk, requested a chunk ahead
@@ -959,7 +976,14 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     auto src = [&](int i) -> const Node* {
       return pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gidx(i), sm.pool);
     };
-    const int total = pfsp_phase_a_wf<NJ, M>(a, sm, nvalid, src);
+    // machine-parallel prefix replay from 10 machines; with 5 the serial replay is
+    // only 5 steps per prefix job and the wavefront's shuffles cost more (ta010 LB2
+    // 4.2 -> 5.7 ms)
+    int total;
+    if constexpr (M >= 10)
+      total = pfsp_phase_a_wf<NJ, M>(a, sm, nvalid, src);
+    else
+      total = pfsp_phase_a<NJ, M, 2>(a, sm, nvalid, src);
     if (timed) {
       const unsigned long long c = clock64();
       tm[0] += c - tc;
@@ -1219,6 +1243,11 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     atomicMax(&a.dbg_time[5], tot);
     atomicAdd(&a.dbg_time[6], tot);
     if (nchunks_done) atomicAdd(&a.dbg_time[7], 1ull);
+  }
+  if (a.dbg_blk && tid == 0) {
+    a.dbg_blk[3 * blockIdx.x] = t_entry;
+    a.dbg_blk[3 * blockIdx.x + 1] = t_pro;
+    a.dbg_blk[3 * blockIdx.x + 2] = wall_clock64();
   }
 }
 

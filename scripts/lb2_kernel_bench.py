@@ -20,11 +20,9 @@ from dist_gpu_accelerated_tree_search_amd.ops import hip
 
 VARIANTS = [
     ("plain walk, blocked chunks", 1, {"TTS_LB2_PIPE": "0", "TTS_LB2_DYN": "0", "TTS_LB2_STRIDE": "0"}),
-    ("pipelined, blocked chunks", 1, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "0", "TTS_LB2_STRIDE": "0"}),
-    ("pipelined, blocked, dyn deal", 1, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "1", "TTS_LB2_STRIDE": "0"}),
-    ("pipelined, strided chunks", 1, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "0", "TTS_LB2_STRIDE": "1"}),
     ("packed 2-child, blocked", 4, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "0", "TTS_LB2_STRIDE": "0"}),
     ("packed 2-child, strided", 4, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "0", "TTS_LB2_STRIDE": "1"}),
+    ("packed 2-child, strided, dyn", 4, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "1", "TTS_LB2_STRIDE": "1"}),
 ]
 
 
@@ -52,6 +50,14 @@ def main():
                   f"B1 {t['clk_b1']:.0f} B2 {t['clk_b2']:.0f} C {t['clk_c']:.0f} ({t['chunks']:.0f} chunks); "
                   f"workgroup clocks max {t['clk_block_max']:.0f} mean {t['clk_block_mean']:.0f} (grid {t['grid']:.0f})",
                   flush=True)
+            tl = t["timeline_us"]
+            if len(tl):
+                ends = np.sort(tl[:, 2])
+                print(f"    workgroups (us from the first entry): entry max {tl[:, 0].max():.1f}, prologue "
+                      f"mean {np.mean(tl[:, 1] - tl[:, 0]):.1f} max {np.max(tl[:, 1] - tl[:, 0]):.1f}, exit "
+                      f"p10 {ends[len(ends) // 10]:.1f} p50 {ends[len(ends) // 2]:.1f} p90 {ends[9 * len(ends) // 10]:.1f} "
+                      f"max {ends[-1]:.1f}; busy share {np.sum(tl[:, 2] - tl[:, 0]) / (len(tl) * ends[-1]):.2f}",
+                      flush=True)
             for k in env:
                 os.environ.pop(k, None)
 
