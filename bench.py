@@ -54,7 +54,7 @@ def main() -> int:
 
     from dist_gpu_accelerated_tree_search_amd.models.pfsp import EngineOptions, PfspModel
     from dist_gpu_accelerated_tree_search_amd.parallel.comm import Comm
-    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig, DistSolver, distributed_solve
+    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig, DistSolver
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
@@ -67,17 +67,13 @@ def main() -> int:
     cfg = DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws)
     golden = GOLDEN.get((a.inst, a.lb)) if a.ub == 1 else None
 
-    # N > 1: one native call per solve (warm-up, split, rounds, reductions: runtime.DistSolver);
-    # N = 1: one fused engine solve (distributed_solve's world-1 path, no rounds)
-    solver = DistSolver(model, engine, comm, cfg, window=a.max_parents) if comm.world > 1 else None
+    # one native call per solve (runtime.DistSolver): warm-up, split, rounds and reductions
+    # at N > 1; at N = 1 the warm-up and the engine's fused solve, no interpreter between
+    solver = DistSolver(model, engine, comm, cfg, window=a.max_parents)
 
     def step():
-        if solver is not None:
-            raw = solver.solve_raw(a.ub)
-            got = (raw[1], raw[2], raw[0])
-        else:
-            r = distributed_solve(model, engine, comm, ub=a.ub, cfg=cfg, window=a.max_parents)
-            raw, got = r, (r.tree, r.sol, r.best)
+        raw = solver.solve_raw(a.ub)
+        got = (raw[1], raw[2], raw[0])
         if golden and got != golden:
             raise SystemExit(f"wrong result {got} != golden {golden}")
         return raw, got[0]
@@ -93,7 +89,7 @@ def main() -> int:
         tree += t
     comm.barrier()
     dt_local = time.perf_counter() - t0
-    last = solver.result(*raw) if solver is not None else raw
+    last = solver.result(*raw)
     dt = float(comm.allgather_f64([dt_local]).max())
     value = tree / dt
     if comm.rank == 0:

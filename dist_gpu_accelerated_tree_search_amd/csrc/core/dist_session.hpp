@@ -55,13 +55,40 @@ struct DistSolveResult {
 
 // Every rank: the same warm-up to `warm_target` nodes, the split armed at `split_min`
 // pool nodes (IEngine::set_split), the rounds, then global counts (Step-1 counts once).
+// A world of one is the engine's fused solve from the warm-up (bench.py at N = 1).
 inline DistSolveResult dist_solve_split(IEngine& e, RoundControl& ctl, const DistOptions& o, const WarmupFn& warm,
                                         int best, size_t warm_target, size_t split_min, const TransferFn& xfer,
                                         const RoundHook& hook) {
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
   WarmupResult w = warm(best, warm_target);
-  if (ctl.world() > 1) e.set_split(ctl.rank(), ctl.world(), split_min);
+  if (ctl.world() == 1) {
+    // one rank: the engine's own fused solve (no rounds, no control plane)
+    const auto t1 = clock::now();
+    const EngineStats st = e.solve_from(w.nodes.data(), w.n, w.best);
+    const auto t2 = clock::now();
+    DistSolveResult r;
+    r.best = std::min(st.best, w.best);
+    r.tree = w.tree + st.tree;
+    r.sol = w.sol + st.sol;
+    r.t_init = std::chrono::duration<double>(t1 - t0).count();
+    r.t_search = std::chrono::duration<double>(t2 - t1).count();
+    r.elapsed = std::chrono::duration<double>(t2 - t0).count();
+    DistOutcome& o1 = r.outcome;
+    o1.best = r.best;
+    auto one = [](auto& v, auto x) { v.assign(1, x); };
+    one(o1.tree, st.tree);
+    one(o1.sol, st.sol);
+    for (auto* v : {&o1.sent, &o1.received, &o1.transfers_in, &o1.transfers_out, &o1.steals, &o1.success_steals,
+                    &o1.idle_rounds, &o1.early_rounds, &o1.dropped})
+      one(*v, 0ull);
+    one(o1.t_run, st.t_run);
+    one(o1.t_memcpy, st.t_memcpy);
+    one(o1.t_malloc, st.t_malloc);
+    for (auto* v : {&o1.t_comm, &o1.t_idle, &o1.t_termination, &o1.t_load_bal}) one(*v, 0.0);
+    return r;
+  }
+  e.set_split(ctl.rank(), ctl.world(), split_min);
   e.begin(w.nodes.data(), w.n, w.best);
   const auto t1 = clock::now();
   DistSolveResult r;

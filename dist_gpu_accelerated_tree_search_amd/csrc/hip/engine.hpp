@@ -69,7 +69,9 @@ class DeviceEngine final : public IEngine {
     }
     TTS_HIP_CHECK(hipMalloc(&d_ctl_, sizeof(dev::PoolCtl)));
     TTS_HIP_CHECK(hipHostMalloc(&h_ctl_, sizeof(dev::PoolCtl), hipHostMallocDefault));
-    TTS_HIP_CHECK(hipHostMalloc(&h_up_, sizeof(dev::PoolCtl), hipHostMallocDefault));
+    // control-block upload, followed by a pinned staging area for begin()'s nodes (a
+    // pageable source would make the node copy synchronous and staged by the runtime)
+    TTS_HIP_CHECK(hipHostMalloc(&h_up_, kUpBytes + kStageNodes * sizeof(Node), hipHostMallocDefault));
     for (int m = 0; m < 2; ++m) {
       TTS_HIP_CHECK(
           hipHostMalloc(&h_mirror_[m], sizeof(dev::PoolCtl), hipHostMallocMapped | hipHostMallocCoherent));
@@ -404,8 +406,15 @@ class DeviceEngine final : public IEngine {
     h_ctl_->slot[0].nch = 0;
     h_ctl_->pend_children = h_ctl_->pend_leaves = h_ctl_->pend_internal = 0;
     h_ctl_->overflow = 0;
-    ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
-    upload_ctl();
+    if (n <= kStageNodes) {
+      TTS_HIP_CHECK(hipEventSynchronize(up_done_));  // the previous upload has read the staging area
+      Node* stage = reinterpret_cast<Node*>(reinterpret_cast<char*>(h_up_) + kUpBytes);
+      std::memcpy(stage, nodes, n * sizeof(Node));
+      ring_write_top(stage, n, hipMemcpyHostToDevice);
+    } else {
+      ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
+    }
+    upload_ctl();  // records up_done_ after both copies
     fresh_ = true;
   }
 
@@ -822,7 +831,9 @@ class DeviceEngine final : public IEngine {
   int* d_lcnt_[2] = {nullptr, nullptr};
   dev::PoolCtl* d_ctl_ = nullptr;
   dev::PoolCtl* h_ctl_ = nullptr;
-  dev::PoolCtl* h_up_ = nullptr;
+  dev::PoolCtl* h_up_ = nullptr;  // + staging for up to kStageNodes nodes at kUpBytes
+  static constexpr size_t kUpBytes = (sizeof(dev::PoolCtl) + 255) & ~size_t(255);
+  static constexpr size_t kStageNodes = 4096;
   dev::PoolCtl* h_mirror_[2] = {nullptr, nullptr};
   dev::PoolCtl* d_mirror_[2] = {nullptr, nullptr};
   hipEvent_t graph_done_[2] = {nullptr, nullptr};

@@ -36,6 +36,13 @@ for step in "$@"; do
           -- python3 scripts/profile_workload.py "$wl" > "$out/trace_$wl.log" 2>&1 ) || { tail -20 "$out/trace_$wl.log"; exit 1; }
       python3 scripts/overlap.py "$out/trace_$wl" > "$out/overlap_$wl.txt"; rm -rf "$out/trace_$wl"
       grep -v "^W20\|^E20\|amdgpu.ids" "$out/trace_$wl.log" | tail -2; cat "$out/overlap_$wl.txt" ;;
+    ktrace:*)  # ktrace:<workload>: kernel trace only, timeline of the last solve
+      wl="${step#ktrace:}"
+      ( cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
+        timeout -k 10 150 rocprofv3 --kernel-trace -d "$out/ktrace_$wl" -o run --output-format csv \
+          -- python3 scripts/profile_workload.py "$wl" > "$out/ktrace_$wl.log" 2>&1 ) || { tail -20 "$out/ktrace_$wl.log"; exit 1; }
+      python3 scripts/solve_timeline.py "$out/ktrace_$wl" 80 > "$out/timeline_$wl.txt"; rm -rf "$out/ktrace_$wl"
+      tail -3 "$out/timeline_$wl.txt" ;;
     py:*)  # py:<script.py>: any probe script, output to <out>/<script>.txt
       sc="${step#py:}"; nm=$(basename "$sc" .py)
       timeout -k 10 300 python -u "$sc" > "$out/$nm.txt" 2>&1 || { tail -20 "$out/$nm.txt"; exit 1; }

@@ -245,10 +245,11 @@ def test_in_search_split_cpu(world, per_rank):
         assert per[1:] == [0] * (world - 1)
 
 
-@pytest.mark.parametrize("world,problem", [(2, "pfsp"), (3, "pfsp"), (4, "nqueens")])
+@pytest.mark.parametrize("world,problem", [(1, "pfsp"), (2, "pfsp"), (3, "pfsp"), (4, "nqueens")])
 def test_native_session_solves(world, problem):
     # runtime.DistSolver: warm-up, split, rounds and reductions in one native call per
-    # solve (bench.py at N > 1); repeated solves on one session stay golden
+    # solve (bench.py); world 1 is the engine's fused solve; repeated solves on one
+    # session stay golden
     spec = {"problem": problem, "inst": 14, "lb": 0, "N": 11, "backend": "cpu", "session": True, "repeat": 3}
     res = spawn_local(world, solve_rank, (spec,), timeout=300)
     gold = GOLD if problem == "pfsp" else (166925, 2680)
