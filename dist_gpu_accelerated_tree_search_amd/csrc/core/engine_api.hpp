@@ -28,6 +28,14 @@ struct EngineConfig {
   int narrow_bp = 16;                    // narrow local DFS for windows of <= this many parents per workgroup
   int narrow_steps = 0;                  // ... up to this many steps per chunk (<= 1: off; measured slower)
   int narrow_cap = 512;                  // ... while the chunk's stack holds <= this many nodes
+  // persistent iterations (kernels that have them): a pool of at least persist_min parents
+  // is searched to the end inside one kernel by persist_wg workgroups sharing work.
+  // Off by default: measured slower than level-per-kernel iterations on every tree tried
+  // (profiles/r2/persist.md); TTS_PERSIST_MIN turns it on.
+  size_t persist_min = 0;                // 0: off
+  int persist_us = 2000;                 // budget of one persistent iteration
+  int persist_wg = 0;                    // 0: min(grid, parent-window chunks / 2)
+  int persist_dmin = 64;                 // a donor splits stacks of at least this many nodes
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };
@@ -39,6 +47,10 @@ struct EngineStats {
   size_t pinned_bytes = 0;  // pinned host spill blocks held
   double t_run = 0, t_memcpy = 0, t_malloc = 0;
   size_t device_nodes = 0, host_nodes = 0, capacity = 0;
+  // persistent iterations (cumulative since the engine was made): workgroup steps,
+  // donations between workgroups, idle waits, microseconds spent waiting (summed)
+  unsigned long long p_steps = 0, p_donations = 0, p_waits = 0;
+  double p_wait_us = 0;
 };
 
 // Type-erased interface used by the Python bindings and the native CLIs.

@@ -31,9 +31,23 @@ struct PfspTraits {
   static constexpr int kChildrenPerChunk = G::SLOT;  // slot region per chunk
   static constexpr int kMaxChildren = NJ;            // children per parent (one level)
   static constexpr int kLocalSteps = G::LT;
+  static constexpr bool kPersist = G::LT > 1;  // persistent iterations (the LB1 register path)
   static constexpr int kMaxChunks = G::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
+  }
+  // the kernel with persistent iterations (kPersist only)
+  static void launch_persist(const Args& a, int t, int grid, hipStream_t s) {
+    if constexpr (kPersist)
+      hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK, true>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
+  }
+  static int blocks_per_cu_persist() {
+    int n = 0;
+    if constexpr (kPersist)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_expand_kernel<NJ, M, LBK, true>, dev::kBlock, 0) !=
+          hipSuccess)
+        return 1;
+    return n;
   }
   static void flatten(const dev::PoolArgs<Node>& pa, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::SLOT, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,

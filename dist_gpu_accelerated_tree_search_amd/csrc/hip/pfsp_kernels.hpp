@@ -481,7 +481,7 @@ __device__ inline void pfsp_lb1_parent(const PfspArgs<NJ, M>& a, Smem& sm, int p
 // state slot t%3, buffer parity t%2.
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
-template <int NJ, int M>
+template <int NJ, int M, bool PK = false>
 __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 
 template <int NJ, int M, bool PACK, bool PS, bool PK = false>
@@ -492,8 +492,13 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 // spills); LB2 is bounded by its LDS footprint instead (4 workgroups per CU for
 // 50 x 20), and the packed-walk kernel (LBK 5) is held to the 128 VGPRs of 4 waves
 // per SIMD (its unrolled walk would otherwise take 130).
-template <int NJ, int M, int LBK>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK == 5 ? 4 : LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
+//
+// PK: the same kernel with persistent iterations compiled in (lb1_small_persist, the
+// LB1 register path only), held to 4 waves per SIMD (128 VGPRs): its work-sharing loop
+// does not fit the plain kernel's budget without spills, and the persistent grid is 4
+// workgroups per CU anyway. The engine replays graphs of it when persistence is on.
+template <int NJ, int M, int LBK, bool PK = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PK ? 4 : LBK == 5 ? 4 : LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
 void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
     pfsp_expand_lb2<NJ, M, false, false>(a, t);
@@ -506,7 +511,7 @@ void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   else if constexpr (LBK == 5)
     pfsp_expand_lb2<NJ, M, false, false>(a, t);  // (job sets of one word only)
   else if constexpr (sizeof(PfspNode<NJ>) == 32)
-    pfsp_expand_lb1_small<NJ, M>(a, t);
+    pfsp_expand_lb1_small<NJ, M, PK>(a, t);
   else
     pfsp_expand_lb1<NJ, M>(a, t);
 }
@@ -1277,13 +1282,17 @@ struct PfspSmemLB1s {
   int scan[kBlock / kWave];
   uint4 mid[kBlock][2];  // level-1 survivors of a two-level chunk
   PoolSmem<G::MAXCHUNKS> pool;
+  int bc[12];            // persistent iterations: thread 0 -> workgroup broadcasts, thread 0 state
+  u64 bq;
+  u64 dl[3];             // persistent iterations: budget deadline, watchdog deadline, ticks waited (thread 0)
 };
 
 // Bounds of every child of the parent held in w (valid lanes only); calls
 // emit(k, lb) for each child position k (static after unrolling).
 template <int NJ, int M, class Emit>
-__device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const uint16_t (*ptab)[PfspConsts<M>::MS],
+__device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const PfspSmemLB1s<NJ, M>& sm,
                                         const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], Emit emit) {
+  const auto& ptab = sm.ptab;
   const int d = static_cast<int>(w[0] & 0xffu);
   // r[m] = unscheduled work on machine m + its min tail: the tail is folded in
   // once per parent instead of once per child and machine
@@ -1327,10 +1336,31 @@ __device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const uint16_t
   }
 }
 
+__device__ inline void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// One 32-B node store, plain or write-through (8-B agent-scope stores = sc1: the line
+// leaves this XCD's L2, so a later writer on another XCD is never shadowed by it).
+__device__ inline void st_node(uint4* dst, const uint4& x0, const uint4& x1, bool wt) {
+  if (wt) {
+    u64* d = reinterpret_cast<u64*>(dst);
+    __hip_atomic_store(d + 0, (static_cast<u64>(x0.y) << 32) | x0.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 1, (static_cast<u64>(x0.w) << 32) | x0.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 2, (static_cast<u64>(x1.y) << 32) | x1.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 3, (static_cast<u64>(x1.w) << 32) | x1.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    dst[0] = x0;
+    dst[1] = x1;
+  }
+}
+__device__ inline u64 uni64(u64 x) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(x));
+  const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(x >> 32));
+  return (static_cast<u64>(hi) << 32) | lo;
+}
+
 // Children of the parent held in w whose positions are set in surv, written as
 // consecutive 32-B nodes from dst (node words in registers, element 0 = depth).
 template <int NJ>
-__device__ inline void emit_children(const uint32_t (&w)[8], uint32_t surv, uint4* dst) {
+__device__ inline void emit_children(const uint32_t (&w)[8], uint32_t surv, uint4* dst, bool wt = false) {
   const int d = static_cast<int>(w[0] & 0xffu);
   const uint32_t jd = node_byte<NJ>(w, 1 + d);
   uint32_t base[8];
@@ -1345,8 +1375,13 @@ __device__ inline void emit_children(const uint32_t (&w)[8], uint32_t surv, uint
     for (int i = 0; i < 8; ++i) c[i] = base[i];
     node_set<NJ>(c, 1 + d, node_byte<NJ>(w, 1 + k));
     node_set<NJ>(c, 1 + k, jd);
-    dst[0] = make_uint4(c[0], c[1], c[2], c[3]);
-    dst[1] = make_uint4(c[4], c[5], c[6], c[7]);
+    const uint4 x0 = make_uint4(c[0], c[1], c[2], c[3]), x1 = make_uint4(c[4], c[5], c[6], c[7]);
+    if (wt) {
+      st_node(dst, x0, x1, true);
+    } else {
+      dst[0] = x0;
+      dst[1] = x1;
+    }
     dst += 2;
   }
 }
@@ -1382,7 +1417,7 @@ __device__ inline void lb1_small_two_level(const PfspArgs<NJ, M>& a, PfspSmemLB1
     int nsurv = 0, nleaf = 0;
     if (valid) {
       const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-      lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
         if (leaf) {
           ++nleaf;
           if (lb < best) atomicMin(&pa.ctl->best.v, lb);
@@ -1403,7 +1438,7 @@ __device__ inline void lb1_small_two_level(const PfspArgs<NJ, M>& a, PfspSmemLB1
       w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
       w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
       const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-      lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
         if (leaf) {
           ++nleaf;
           if (lb < best) atomicMin(&pa.ctl->best.v, lb);
@@ -1473,7 +1508,7 @@ __device__ inline void lb1_small_local(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ
       int nsurv = 0;
       if (valid) {
         const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-        lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+        lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
           if (leaf) {
             ++nleaf;
             if (lb < best) atomicMin(&pa.ctl->best.v, lb);
@@ -1502,7 +1537,347 @@ __device__ inline void lb1_small_local(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent iteration (v.persist, pool_device.hpp): the whole window is explored in
+// this kernel. Workgroup g < persist_wg runs a depth-first search on its own stack —
+// persist_r consecutive chunk slots of the output buffer, [bot, top) — popping up to
+// kBlock nodes per step (one per thread, bounds by lb1_small_parent) and pushing the
+// survivors on top. An empty stack takes the workgroup's next window slice (slices g,
+// g + P, g + 2P, ... of `grab` parents: no shared counter). With none left the
+// workgroup goes idle and waits for a donation: it counts itself idle in its shard,
+// posts an odd generation in box[g].want and polls box[g].mail. A workgroup holding at
+// least persist_dmin nodes probes 16 random boxes per step (issued with its pops); on an
+// odd one it claims it (CAS to even, counting the receiver busy), copies the bottom half
+// of its stack (the shallowest nodes, the largest subtrees) into the receiver's slots
+// and publishes {generation, count} in its mail. Stack writes are write-through (sc1,
+// persist_wt) so no XCD's L2 holds a dirty line of another workgroup's slots: payload,
+// every wave's vmcnt(0), barrier, flag; the receiver polls, acquires, barriers
+// (cdna_hip_programming.md G16 R1). The search ends when every started workgroup is
+// idle (a consistent snapshot of the shards), or at the budget / a full stack (stop):
+// then each workgroup's untaken slices go on its stack, and the stacks are the chunks'
+// output, exactly as a local DFS iteration leaves them. Counts go to the workgroup's
+// record pst[t & 1][g] (plain stores, no shared counter): a stack pop is an explored
+// tree node, minus the untaken slices put back (counted when they were pushed).
+__device__ inline int persist_box_gen(u64 m) { return static_cast<int>(m >> 32); }
+
+// Termination check (thread 0): two identical collects of the shards, all idle.
+__device__ inline bool persist_all_idle(const PersistWs* ws) {
+  u64 a[kPersistShards], b[kPersistShards];
+#pragma unroll
+  for (int i = 0; i < kPersistShards; ++i) a[i] = __hip_atomic_load(&ws->sh[i].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool idle = true;
+#pragma unroll
+  for (int i = 0; i < kPersistShards; ++i) idle &= ((a[i] >> 16) & 0xffffu) == (a[i] & 0xffffu);
+  if (!idle) return false;
+#pragma unroll
+  for (int i = 0; i < kPersistShards; ++i) b[i] = __hip_atomic_load(&ws->sh[i].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool same = true;
+#pragma unroll
+  for (int i = 0; i < kPersistShards; ++i) same &= a[i] == b[i];
+  return same;
+}
+
 template <int NJ, int M>
+__device__ inline void lb1_small_persist(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ, M>& sm, const IterView& v, int t,
+                                         int best0) {
+  using G = PfspGeom<NJ, 1>;
+  using Node = PfspNode<NJ>;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const auto& pa = a.pool;
+  const int me = blockIdx.x;
+  const int P = pa.persist_wg;
+  if (me >= P) return;
+  PersistWs* const ws = pa.pws + (t & 1);
+  PersistBox* const box = pa.box;
+  Node* const bout = pa.buf[(t & 1) ^ 1];
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  const int R = pa.persist_r;
+  const int cap = R * G::SLOT;
+  uint4* const stk = reinterpret_cast<uint4*>(bout + static_cast<size_t>(me) * cap);
+  const u64 B = v.B;
+  const bool wt = pa.persist_wt != 0;
+  u64* const shard = &ws->sh[me % kPersistShards].v;
+  // window slices: me, me + P, ...; room for the untaken ones is kept on the stack
+  const int grab = static_cast<int>(min(static_cast<u64>(kBlock), max(1ull, (B + P - 1) / P)));
+  const u64 nsl = (B + grab - 1) / grab;
+  u64 sl = static_cast<u64>(me);
+  const int mine = sl < nsl ? static_cast<int>((nsl - 1 - sl) / P + 1) : 0;
+  const int lim = cap - mine * grab;  // pushes stay below this
+  // thread 0's state lives in LDS (registers are the LB1 loop's): sm.bc[9] want
+  // generation (even between waits), sm.bc[11] waits, sm.dl = budget / watchdog
+  // deadlines and ticks spent waiting
+  if (tid == 0) {
+    __hip_atomic_fetch_add(shard, (1ull << 32) | (1ull << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm.bc[9] = static_cast<int>(__hip_atomic_load(&box[me].want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    sm.bc[11] = 0;
+    sm.bc[10] = best0;
+    const u64 deadline = wall_clock64() + pa.persist_ticks;
+    sm.dl[0] = deadline;
+    sm.dl[1] = deadline + 10000000ull;  // +100 ms at 100 MHz: only a broken protocol gets here
+    sm.dl[2] = 0;
+  }
+  int bot = 0, top = 0;  // uniform
+  u64 popped = 0;        // uniform
+  int steps = 0, ndon = 0;
+  int nleaf = 0;
+  int best = best0;
+  bool full = false;
+  // [bot, top) -> [0, top - bot): blocks in ascending order, each read before written
+  auto compact = [&]() {
+    const int n = top - bot;
+    for (int base = 0; base < n; base += kBlock) {
+      const int i = base + tid;
+      uint4 x0, x1;
+      if (i < n) {
+        x0 = stk[2 * (bot + i)];
+        x1 = stk[2 * (bot + i) + 1];
+      }
+      __syncthreads();
+      if (i < n) st_node(stk + 2 * i, x0, x1, wt);
+      __syncthreads();
+    }
+    top = n;
+    bot = 0;
+  };
+  for (;;) {
+    int n = top - bot;
+    u64 g0 = 0;
+    int npop;
+    bool from_stack = n > 0;
+    if (!from_stack) {
+      bot = top = 0;
+      if (sl < nsl) {
+        g0 = sl * static_cast<u64>(grab);
+        npop = static_cast<int>(min(static_cast<u64>(grab), B - g0));
+        sl += static_cast<u64>(P);
+      } else {
+        // idle: wait for a donation, the end of the search, or the stop
+        vm_drain();
+        __syncthreads();
+        if (tid == 0) {
+          int got = 0;
+          const unsigned g = static_cast<unsigned>(sm.bc[9]) + 1;
+          const u64 hard = sm.dl[1];
+          const u64 t_wait = wall_clock64();
+          sm.bc[11] += 1;
+          if (!wt) {  // no dirty line of these slots may shadow a donation
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            vm_drain();
+          }
+          __hip_atomic_fetch_add(shard, (1ull << 32) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          vm_drain();  // counted idle before a donor can see the request
+          __hip_atomic_store(&box[me].want, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (unsigned spin = 0;; ++spin) {
+            const u64 m = __hip_atomic_load(&box[me].mail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (static_cast<unsigned>(persist_box_gen(m)) == g + 1) {
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+              vm_drain();
+              got = static_cast<int>(m & 0xffffffffu);
+              sm.bc[9] = static_cast<int>(g + 1);
+              break;
+            }
+            const u64 now = wall_clock64();
+            // workgroup 0 alone watches the shards; when every started workgroup is
+            // idle it tells each one through its box
+            bool end = false;
+            if (me == 0 && (spin & 3) == 3 && persist_all_idle(ws)) {
+              for (int j = 1; j < P; ++j)
+                __hip_atomic_store(&box[j].stop, v.pid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              end = true;
+            }
+            const bool stop = end || now > sm.dl[0] ||
+                              __hip_atomic_load(&box[me].stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v.pid;
+            if (stop || now > hard) {
+              unsigned e = g;
+              if (__hip_atomic_compare_exchange_strong(&box[me].want, &e, g + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)) {
+                sm.bc[9] = static_cast<int>(g + 1);
+                if (now > hard) __hip_atomic_store(&pa.ctl->perr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+              // claimed: the donor's mail is on its way
+              if (now > hard + 10000000ull) {
+                __hip_atomic_store(&pa.ctl->perr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+            }
+            __builtin_amdgcn_s_sleep(4);
+          }
+          sm.dl[2] += wall_clock64() - t_wait;
+          sm.bc[6] = got;
+        }
+        __syncthreads();
+        const int got = __builtin_amdgcn_readfirstlane(sm.bc[6]);
+        __syncthreads();
+        if (got <= 0) break;
+        top = got;
+        n = got;
+        from_stack = true;
+      }
+    }
+    if (from_stack) {
+      // room for the children of a full pop (at most NJ - 1 per stack node)
+      if (top + kBlock * (NJ - 1) > lim && bot > 0) compact();
+      npop = min(min(n, kBlock), (lim - top) / (NJ - 1));
+      if (npop < 1) {
+        full = true;
+        break;
+      }
+    }
+    uint32_t w[8];
+    const bool valid = tid < npop;
+    if (valid) {
+      const uint4* src = from_stack
+                             ? stk + 2 * (top - npop + tid)
+                             : reinterpret_cast<const uint4*>(
+                                   pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool));
+      const uint4 x0 = src[0], x1 = src[1];
+      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+    }
+    // in flight with the pops, parked in LDS (no register holds them across the
+    // bounds): the stop word and the incumbent (thread 0); with enough nodes to
+    // share, 16 random boxes (wave 0): the first waiting one is the candidate
+    // (staging slots bc[3], bc[10], bc[4], bc[7]: read by thread 0 only, after the scan's
+    // barriers, when every wave has read the previous step's broadcasts)
+    if (tid == 0) {
+      sm.bc[3] = __hip_atomic_load(&box[me].stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v.pid;
+      if ((steps & 15) == 15)  // the incumbent's line is shared: read now and then
+        sm.bc[10] = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const bool share = top - npop * from_stack - bot >= pa.persist_dmin;
+    if (share && tid < kWave) {
+      unsigned h = static_cast<unsigned>(me) * 0x9e3779b9u + static_cast<unsigned>(steps) * 0x85ebca6bu +
+                   static_cast<unsigned>(lane) * 0xc2b2ae35u;
+      h ^= h >> 15;
+      h *= 0x2c1b3c6du;
+      h ^= h >> 12;
+      const int r = static_cast<int>(h % static_cast<unsigned>(P));
+      unsigned wv = 0;
+      if (lane < 16 && r != me) wv = __hip_atomic_load(&box[r].want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const u64 odd = __ballot(wv & 1u);
+      const int first = odd ? __ffsll(static_cast<long long>(odd)) - 1 : -1;
+      if (lane == 0) sm.bc[4] = -1;
+      if (first >= 0 && lane == first) {
+        sm.bc[4] = r;
+        sm.bc[7] = static_cast<int>(wv);
+      }
+    }
+    if (from_stack) {
+      top -= npop;
+      popped += static_cast<u64>(npop);
+    }
+    ++steps;
+    uint32_t surv = 0;
+    int nsurv = 0;
+    if (valid) {
+      const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
+      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
+        if (leaf) {
+          ++nleaf;
+          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+        } else if (lb < best) {
+          ++nsurv;
+          surv |= 1u << k;
+        }
+      });
+    }
+    int tot = 0;
+    const int off = block_exclusive_scan(nsurv, sm.scan, &tot);
+    if (surv) emit_children<NJ>(w, surv, stk + 2 * (top + off), wt);
+    top += __builtin_amdgcn_readfirstlane(tot);
+    if (tid == 0) {
+      // every workgroup keeps its own deadline (nothing shared to poll)
+      const int stop = sm.bc[3] || wall_clock64() > sm.dl[0];
+      sm.bc[0] = stop;
+      sm.bc[2] = sm.bc[10];
+      sm.bc[5] = share ? sm.bc[4] : -1;
+      sm.bc[8] = sm.bc[7];
+    }
+    // pushes visible to the next step's pops (workgroup scope) + the broadcast
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(sm.bc[0])) break;
+    best = min(best, __builtin_amdgcn_readfirstlane(sm.bc[2]));
+    if (__builtin_amdgcn_readfirstlane(sm.bc[5]) >= 0 && top - bot >= pa.persist_dmin) {
+      __syncthreads();  // every wave has read bc[5]
+      if (tid == 0) {
+        const int r = sm.bc[5];
+        unsigned e = static_cast<unsigned>(sm.bc[8]);
+        int rr = -1;
+        if (__hip_atomic_compare_exchange_strong(&box[r].want, &e, e + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          // the receiver counts busy from now on (version + 1, idle - 1)
+          __hip_atomic_fetch_add(&ws->sh[r % kPersistShards].v, (1ull << 32) - 1ull, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          rr = r;
+          sm.bc[8] = static_cast<int>(e + 1);
+        }
+        sm.bc[1] = rr;
+      }
+      __syncthreads();
+      const int r = __builtin_amdgcn_readfirstlane(sm.bc[1]);
+      if (r >= 0) {
+        const int h = (top - bot) / 2;
+        uint4* const dst = reinterpret_cast<uint4*>(bout + static_cast<size_t>(r) * cap);
+        for (int x = tid; x < h; x += kBlock) st_node(dst + 2 * x, stk[2 * (bot + x)], stk[2 * (bot + x) + 1], wt);
+        vm_drain();
+        __syncthreads();
+        if (tid == 0) {
+          if (!wt) {  // write-through payload: drained stores are already past every L2
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            vm_drain();
+          }
+          const u64 m = (static_cast<u64>(static_cast<unsigned>(sm.bc[8])) << 32) | static_cast<unsigned>(h);
+          __hip_atomic_store(&box[r].mail, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bot += h;
+        ++ndon;
+      }
+    }
+  }
+  if (full && tid == 0) {  // the first to find a full stack tells every workgroup
+    int e = 0;
+    if (__hip_atomic_compare_exchange_strong(&ws->stop.v, &e, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      for (int j = 0; j < P; ++j) __hip_atomic_store(&box[j].stop, v.pid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // leave: the stack at the slot base, then this workgroup's untaken window slices on
+  // top (room was kept for them); they were counted when pushed, so they come off the
+  // tree count again (the next iteration counts its input chunks)
+  if (bot > 0) compact();
+  u64 back = 0;
+  for (; sl < nsl; sl += static_cast<u64>(P)) {
+    const u64 x = sl * static_cast<u64>(grab);
+    const int k = static_cast<int>(min(static_cast<u64>(grab), B - x));
+    if (tid < k) {
+      const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, x + tid, sm.pool));
+      const uint4 x0 = src[0], x1 = src[1];
+      stk[2 * (top + tid)] = x0;
+      stk[2 * (top + tid) + 1] = x1;
+    }
+    top += k;
+    back += static_cast<u64>(k);
+  }
+  for (int j = tid; j < R; j += kBlock) {
+    cnt_out[me * R + j] = max(0, min(G::SLOT, top - j * G::SLOT));
+    lcnt_out[me * R + j] = 0;
+  }
+  int leaves = 0;
+  (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
+  if (tid == 0) {
+    u64* rec = pa.pst + (static_cast<size_t>(t & 1) * P + me) * kPstWords;
+    rec[0] = popped - back;
+    rec[1] = static_cast<u64>(leaves);
+    rec[2] = static_cast<u64>(steps);
+    rec[3] = static_cast<u64>(ndon);
+    rec[4] = static_cast<u64>(sm.bc[11]);
+    rec[5] = sm.dl[2];
+  }
+}
+
+template <int NJ, int M, bool PK>
 __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
   using G = PfspGeom<NJ, 1>;
   using Node = PfspNode<NJ>;
@@ -1519,7 +1894,7 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
     const int x = tid + i * kBlock;
     ptv[i] = x < a.jobs * PfspConsts<M>::MS ? a.ptab[x] : 0;
   }
-  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, PfspSmemLB1s<NJ, M>::BPF, G::LT);
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, PfspSmemLB1s<NJ, M>::BPF, G::LT, PK);
   if (v.B == 0 || v.overflow) return;
   {  // p table -> LDS (visible after the barrier below)
     uint16_t* pt = &sm.ptab[0][0];
@@ -1533,6 +1908,12 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
   pool_spill_leftovers<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, sm.pool);
   __syncthreads();
+  if constexpr (PK) {
+    if (v.persist) {
+      lb1_small_persist<NJ, M>(a, sm, v, t, best);
+      return;
+    }
+  }
   if (v.local) {
     lb1_small_local<NJ, M>(a, sm, v, t, best);
     return;
@@ -1567,7 +1948,7 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
       for (int k = 0; k < NJ; ++k) kmask |= split_keep(v, gi, k) ? (1u << k) : 0u;
     }
     if (valid) {
-      lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) {
+      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
         const bool keep = (kmask >> k) & 1u;
         if (leaf) {
           nleaf += keep;
@@ -1721,7 +2102,7 @@ __global__ __launch_bounds__(kBlock) void pfsp_bounds_kernel(PfspArgs<NJ, M> a) 
       w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
       const int d = static_cast<int>(w[0] & 0xffu);
       int* out = a.bounds_out + a.offsets[i];
-      lb1_small_parent<NJ, M>(a, sm.ptab, w, [&](int k, int lb) { out[k - d] = lb; });
+      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) { out[k - d] = lb; });
     }
   } else if constexpr (LBK != 2) {
     constexpr int VPN = sizeof(Node) / 16;

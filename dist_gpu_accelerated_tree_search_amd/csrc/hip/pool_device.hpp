@@ -37,6 +37,8 @@ struct PoolCtl {
     int nch;    // chunks written by iteration t-1 into buffer t%2
     int sdone;  // armed rank split already done (see split_world)
     int qnext;  // chunk queue of kernels that deal chunks dynamically (LB2); reset by iteration t-1
+    int pers;   // iteration t-1 was persistent: its per-workgroup counts wait in pst[(t-1) & 1]
+    unsigned pid;  // iteration number (+1 per iteration): the epoch of a persistent iteration's stop words
   };
   Slot slot[3];
   // plain counters, updated by workgroup 0 (or the host between launches)
@@ -59,7 +61,40 @@ struct PoolCtl {
   int split_rank;
   int pad0;
   u64 split_min;
+  // persistent iterations: counts of the latest one when it ended a graph (finalize
+  // kernel; kPst* order: tree, sol, then the diagnostics), and the diagnostics so far
+  // (workgroup steps, donations, idle waits, wall-clock ticks spent waiting)
+  u64 pend_p[6];
+  u64 pdiag[4];
+  int perr;           // a persistent iteration's watchdog expired (nodes may be lost)
+  int pad1;
   CtlI32 best;      // incumbent (atomicMin by leaves)
+};
+
+// Work-sharing state of one persistent iteration (two, used by iterations of
+// alternating parity: iteration t works in ws[t & 1], its workgroup 0 clears
+// ws[(t + 1) & 1] for the next one). Workgroup g counts itself in shard g % 8 (each on
+// its own line: one hot word would serialise ~90 atomics/us): {version:32 |
+// started:16 | idle:16}, every update bumps the version. Termination: two collects of
+// the 8 shards that are identical (no update in between: a consistent snapshot) with
+// idle == started in each. A donor counts its receiver busy before it copies, so no
+// work is in flight in such a snapshot.
+constexpr int kPersistShards = 8;
+constexpr int kPstWords = 16;  // per-workgroup count record (one 128-B line): tree, sol, steps, donations, waits, wait ticks
+struct PersistWs {
+  CtlU64 sh[kPersistShards];
+  CtlI32 stop;  // a stack is full: the first to see it tells every workgroup (box stop words)
+};
+// One line per workgroup, polled by it alone (a line polled by every workgroup queues
+// each load behind the others: ~90 per us): its want generation (odd = waiting; a donor
+// claims it by CAS to even), the donor's {generation, count} mail, and the stop word
+// (== the iteration's pid: leave now; written by workgroup 0 when the search is over,
+// or by the workgroup that found a full stack).
+struct alignas(128) PersistBox {
+  unsigned want;
+  unsigned stop;
+  u64 mail;
+  u64 pad[14];
 };
 
 template <class Node>
@@ -79,6 +114,22 @@ struct PoolArgs {
   int narrow_bp;    // narrow local DFS for windows of at most narrow_bp parents per workgroup (0: off)
   int narrow_steps; // ... of up to this many steps per chunk
   int narrow_cap;   // ... while the chunk's stack holds at most this many nodes
+  // Persistent iterations (kernels that implement them, see pool_begin): when the pool
+  // holds at least persist_min parents, persist_wg workgroups each run a depth-first
+  // search on a private stack (persist_r chunk slots) until the whole window's subtrees
+  // are explored or persist_ticks wall-clock ticks have passed, sharing work in the kernel:
+  // an idle workgroup posts an odd generation in want[wg]; a donor claims it (CAS to
+  // even), copies the bottom half of its own stack into the receiver's slots and
+  // publishes {generation, count} in mail[wg] (agent release / acquire).
+  u64 persist_min;  // 0: off
+  u64 persist_ticks;  // budget in wall-clock ticks (s_memrealtime)
+  int persist_wg;
+  int persist_r;
+  int persist_dmin; // smallest stack a donor splits
+  int persist_wt;   // stack writes write-through (sc1): no dirty stack line in any L2, no L2 write-back before a wait
+  PersistWs* pws;   // [2]
+  PersistBox* box;  // [persist_wg]
+  u64* pst;         // [2][persist_wg][kPstWords]: each workgroup's counts, folded by the next iteration / finalize
 };
 
 // Per-chunk leaf word: leaves in the low 16 bits; the high 16 bits count the
@@ -91,7 +142,41 @@ struct PoolSmem {
   int pre[MAXCHUNKS + 1];
   int scan[kBlock / kWave];
   int red[kBlock / kWave];
+  u64 red64[kBlock / kWave][6];
 };
+
+// Sums of the persistent iteration's per-workgroup count records pst[parity] (one
+// workgroup; contains __syncthreads()).
+template <class Node, int MAXCHUNKS>
+__device__ inline void persist_sum(const PoolArgs<Node>& pa, int parity, PoolSmem<MAXCHUNKS>& ps, u64 (&s)[6]) {
+  u64 acc[6] = {0, 0, 0, 0, 0, 0};
+  const u64* rec = pa.pst + static_cast<size_t>(parity) * pa.persist_wg * kPstWords;
+  for (int i = threadIdx.x; i < pa.persist_wg; i += kBlock)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) acc[k] += rec[static_cast<size_t>(i) * kPstWords + k];
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    for (int o = kWave / 2; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) ps.red64[threadIdx.x / kWave][k] = acc[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    s[k] = 0;
+    for (int w = 0; w < kBlock / kWave; ++w) s[k] += ps.red64[w][k];
+  }
+  __syncthreads();
+}
+
+// Workgroup 0 of every iteration: clear the next iteration's work-sharing state.
+template <class Node>
+__device__ inline void persist_clear_next(const PoolArgs<Node>& pa, int t) {
+  if (!pa.pws) return;
+  PersistWs* n = pa.pws + ((t + 1) & 1);
+  if (threadIdx.x < kPersistShards) n->sh[threadIdx.x].v = 0;
+  if (threadIdx.x == kPersistShards) n->stop.v = 0;
+}
 
 // Exclusive prefix of cnt[0..n) into pre[0..n] (pre[n] = total) by one workgroup.
 template <int MAXCHUNKS>
@@ -136,6 +221,8 @@ struct IterView {
   int steps;          // local DFS: steps per chunk at most
   int cap;            // local DFS: no further step once the stack holds more than this
   int srank, sworld;
+  bool persist;       // persistent iteration: work-sharing depth-first search in one kernel
+  unsigned pid;       // iteration number (Slot::pid)
 };
 
 // Does this rank keep child position k of window parent gi? (always, outside the
@@ -165,8 +252,13 @@ template <class Node, int MAXCHUNKS>
 // of its chunk's own slot region — a private stack in L2 — for up to local_steps
 // levels; what is left on the stack is the chunk's output. Several tree levels per
 // dependent kernel, and the next iteration re-deals the stacks over the grid.
+//
+// Persistent iterations (PER, kernels that implement them; pa.persist_min > 0): a
+// window of at least persist_min parents, outside a pending rank split, is explored
+// to the end inside one kernel (or for pa.persist_ticks): persist_wg x persist_r
+// chunks are written (each workgroup's stack left over), no other mode applies.
 __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, PoolSmem<MAXCHUNKS>& ps,
-                                      int BPF = 0, int LT = 1) {
+                                      int BPF = 0, int LT = 1, bool PER = false) {
   const int s_in = t % 3, s_out = (t + 1) % 3;
   const int b_in = t & 1;
   PoolCtl* ctl = pa.ctl;
@@ -176,6 +268,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // ms, profiles/r1/r1q: cold count lines), though ta008 gained 4 %.
   IterView v;
   v.S = ctl->slot[s_in].stack;
+  v.pid = ctl->slot[s_in].pid;
   v.nch_in = ctl->slot[s_in].nch;
   const int done_in = ctl->slot[s_in].sdone;
   v.bot = ctl->bot;
@@ -187,7 +280,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     // and leave — no table staging, no scans, no counter traffic
     v.C = v.B = v.nb = v.ns = v.L = v.Snew = v.bot = 0;
     v.nchunks = 0;
-    v.overflow = v.split = v.fused = v.local = false;
+    v.overflow = v.split = v.fused = v.local = v.persist = false;
     v.bp = BP;
     v.steps = v.cap = 0;
     v.srank = v.sworld = 0;
@@ -195,10 +288,14 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
       ctl->slot[s_out].stack = 0;
       ctl->slot[s_out].nch = 0;
       ctl->slot[s_out].sdone = done_in;
+      ctl->slot[s_out].pers = 0;
+      ctl->slot[s_out].pid = v.pid + 1;
     }
+    if (PER && blockIdx.x == 0) persist_clear_next(pa, t);
     return v;
   }
-  v.C = static_cast<u64>(build_prefix(pa.cnt[b_in], v.nch_in, ps));
+  // uniform by construction: readfirstlane keeps the window arithmetic in SGPRs
+  v.C = static_cast<u64>(__builtin_amdgcn_readfirstlane(build_prefix(pa.cnt[b_in], v.nch_in, ps)));
   v.B = min(v.S + v.C, static_cast<u64>(pa.max_parents));
   const bool armed = v.sworld > 1 && !done_in && v.B > 0;
   // Local DFS when the pool holds a backlog of pa.local_min parents (default: four
@@ -215,8 +312,10 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // as it holds more than pa.narrow_cap nodes (the subtree turned wide).
   const u64 full = static_cast<u64>(gridDim.x) * BP;
   const u64 lmin = pa.local_min > 0 ? static_cast<u64>(pa.local_min) : 4 * full;
-  const bool wide = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= max(lmin, full);
-  const bool narrow = !wide && LT > 1 && pa.narrow_steps > 1 && !armed &&
+  const bool per = PER && pa.persist_min > 0 && !armed && v.S + v.C >= pa.persist_min;
+  v.persist = per;
+  const bool wide = !per && LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= max(lmin, full);
+  const bool narrow = !per && !wide && LT > 1 && pa.narrow_steps > 1 && !armed &&
                       v.B <= static_cast<u64>(gridDim.x) * static_cast<u64>(pa.narrow_bp);
   v.local = wide || narrow;
   v.steps = wide ? pa.local_steps : pa.narrow_steps;
@@ -230,7 +329,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // a pending split needs the whole (replicated) pool inside the window
   const bool bad_split = armed && v.B < v.S + v.C;
   v.split = armed && !bad_split && v.B >= split_min;
-  v.fused = !v.local && BPF > 0 && !armed && v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
+  v.fused = !per && !v.local && BPF > 0 && !armed && v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
   int bp = v.fused ? BPF : BP;
   if (v.local) {
     // spread a window smaller than the grid over every workgroup
@@ -238,7 +337,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     bp = static_cast<int>(min(static_cast<u64>(BP), max(per, 1ull)));
   }
   v.bp = bp;
-  v.nchunks = static_cast<int>((v.B + bp - 1) / bp);
+  v.nchunks = per ? pa.persist_wg * pa.persist_r : static_cast<int>((v.B + bp - 1) / bp);
   const bool overflow = v.overflow;
   v.overflow = overflow || bad_split;
   if (blockIdx.x == 0) {
@@ -252,10 +351,23 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     int lf_total = 0, in_total = 0;
     (void)block_exclusive_scan(lf, ps.red, &lf_total);
     (void)block_exclusive_scan(in, ps.scan, &in_total);
+    // counts of a persistent previous iteration (explored tree, leaves, diagnostics)
+    // (kernels with persistent iterations only: in an engine that has them every
+    // iteration runs such a kernel, and the host folds them before anything else runs)
+    u64 pc[6] = {0, 0, 0, 0, 0, 0};
+    if (PER && ctl->slot[s_in].pers) persist_sum<Node, MAXCHUNKS>(pa, (t + 1) & 1, ps, pc);
     if (threadIdx.x == 0) {
       ctl->slot[s_out].stack = v.overflow ? v.S : v.Snew;
       ctl->slot[s_out].nch = v.overflow ? 0 : v.nchunks;
       ctl->slot[s_out].sdone = (done_in || v.split) ? 1 : 0;
+      ctl->slot[s_out].pers = (!v.overflow && v.persist) ? 1 : 0;
+      ctl->slot[s_out].pid = v.pid + 1;
+      if (PER) {
+        ctl->tree += pc[0];
+        ctl->sol += pc[1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ctl->pdiag[k] += pc[2 + k];
+      }
       if (v.split && v.srank != 0) {
         // everything counted so far was explored identically by every rank: rank 0 keeps it
         ctl->tree = 0;
@@ -271,6 +383,8 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
       if (overflow) ctl->overflow = 1;
       else if (bad_split) ctl->overflow = 2;
     }
+    // the next iteration's work-sharing state (nobody uses it during this one)
+    if (PER) persist_clear_next(pa, t);
   }
   return v;
 }
@@ -379,10 +493,15 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   (void)block_exclusive_scan(c, ps.scan, &ct);
   (void)block_exclusive_scan(l, ps.red, &lt);
   (void)block_exclusive_scan(in, ps.scan, &it);
+  // the graph's last iteration (t = 5, parity 1) was persistent: its counts
+  u64 pc[6] = {0, 0, 0, 0, 0, 0};
+  if (pa.ctl->slot[0].pers) persist_sum<Node, MAXCHUNKS>(pa, 1, ps, pc);
   if (threadIdx.x == 0) {
     pa.ctl->pend_children = static_cast<u64>(ct);
     pa.ctl->pend_leaves = static_cast<u64>(lt);
     pa.ctl->pend_internal = static_cast<u64>(it);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pa.ctl->pend_p[k] = pc[k];
     pa.ctl->seq = seq;
   }
   // publish the whole control block to host-mapped memory: the host reads it
@@ -392,6 +511,7 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   constexpr int kPl = static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4);
   constexpr int kPi = static_cast<int>(offsetof(PoolCtl, pend_internal) / 4);
   constexpr int kSeq = static_cast<int>(offsetof(PoolCtl, seq) / 4);
+  constexpr int kPp = static_cast<int>(offsetof(PoolCtl, pend_p) / 4);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pa.ctl);
   uint32_t* dst = reinterpret_cast<uint32_t*>(pa.mirror);
   for (int i = threadIdx.x; i < static_cast<int>(sizeof(PoolCtl) / 4); i += kBlock) {
@@ -403,6 +523,7 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
     if (i == kPl + 1) x = 0;
     if (i == kPi) x = static_cast<uint32_t>(it);
     if (i == kPi + 1) x = 0;
+    if (i >= kPp && i < kPp + 12) x = static_cast<uint32_t>(pc[(i - kPp) >> 1] >> (((i - kPp) & 1) * 32));
     __hip_atomic_store(dst + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();

@@ -41,7 +41,7 @@ def resources(src):
 
 def main():
     srcs = sys.argv[1:] or sorted(glob.glob("dist_gpu_accelerated_tree_search_amd/csrc/hip/*.hip"))
-    print(f"| kernel | VGPR | SGPR | LDS B | scratch B/lane | waves/SIMD |\n|---|---|---|---|---|---|")
+    print(f"| kernel | VGPR | SGPR | LDS B | scratch B/lane | waves/SIMD | VGPR spill | SGPR spill |\n|---|---|---|---|---|---|---|---|")
     seen = set()
     for s in srcs:
         for r in resources(s):
@@ -49,7 +49,7 @@ def main():
                 continue
             seen.add(r["name"])
             print(f"| {r['name']} | {r.get('vgpr')} | {r.get('sgpr')} | {r.get('lds')} | {r.get('scratch')} | "
-                  f"{r.get('occ')} |")
+                  f"{r.get('occ')} | {r.get('vspill')} | {r.get('sspill')} |")
 
 
 if __name__ == "__main__":
