@@ -59,7 +59,7 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    comm = Comm(use_gpu=(a.backend == "gpu" and a.comm == "nccl"))
+    comm = Comm(use_gpu=(a.backend == "gpu" and a.comm == "nccl"), device=a.device)
     model = PfspModel(a.inst, a.lb)
     opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * (1 << 30)))
     device = (comm.topo.local_rank if a.device is None else a.device) if a.backend == "gpu" else 0

@@ -61,7 +61,8 @@ class Topology:
 class Comm:
     """Process-group wrapper; world == 1 works without any process group."""
 
-    def __init__(self, backend: str | None = None, use_gpu: bool = True, timeout_s: float = 1800.0):
+    def __init__(self, backend: str | None = None, use_gpu: bool = True, timeout_s: float = 1800.0,
+                 device: int | None = None):
         import torch
         import torch.distributed as dist
 
@@ -72,8 +73,10 @@ class Comm:
                              local_world=_env_int("LOCAL_WORLD_SIZE", _env_int("WORLD_SIZE", 1)))
         self.use_gpu = use_gpu
         if use_gpu:
-            torch.cuda.set_device(self.topo.local_rank)
-            self.device = torch.device("cuda", self.topo.local_rank)
+            # device: this rank's GPU (default LOCAL_RANK; tests put several ranks on one)
+            dev = self.topo.local_rank if device is None else int(device)
+            torch.cuda.set_device(dev)
+            self.device = torch.device("cuda", dev)
         else:
             self.device = torch.device("cpu")
         self.backend = backend or ("nccl" if use_gpu else "gloo")
@@ -160,7 +163,7 @@ class Comm:
 
     def _pg_barrier(self) -> None:
         if self.use_gpu and self.backend == "nccl":
-            self.dist.barrier(device_ids=[self.topo.local_rank])
+            self.dist.barrier(device_ids=[self.device.index])
         else:
             self.dist.barrier()
 
