@@ -405,6 +405,7 @@ class DeviceEngine final : public IEngine {
     }
     h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
     for (auto& x : h_ctl_->pend_p) x = 0;
+    for (auto& x : h_ctl_->xacc) x.tree = x.sol = 0;
     for (auto& sl : h_ctl_->slot) sl.pers = 0;
     h_ctl_->best.v = best;
     h_ctl_->bot = 0;
@@ -529,6 +530,10 @@ class DeviceEngine final : public IEngine {
     EngineStats s = stats_;
     s.tree = h_ctl_->tree + h_ctl_->pend_children + h_ctl_->pend_internal + h_ctl_->pend_p[0];
     s.sol = h_ctl_->sol + h_ctl_->pend_leaves + h_ctl_->pend_p[1];
+    for (const auto& x : h_ctl_->xacc) {
+      s.tree += x.tree;
+      s.sol += x.sol;
+    }
     if (h_ctl_->split_world > 1 && !h_ctl_->slot[0].sdone && h_ctl_->split_rank != 0 && dev_total() == 0 &&
         spill_.empty() && refill_n_ == 0)
       s.tree = s.sol = 0;  // the tree died out before the split: every rank explored all of it
@@ -642,6 +647,12 @@ class DeviceEngine final : public IEngine {
       h_ctl_->slot[0].pers = 0;
     }
     for (auto& x : h_ctl_->pend_p) x = 0;
+    // subtrees finished inside iterations (N-Queens)
+    for (auto& x : h_ctl_->xacc) {
+      h_ctl_->tree += x.tree;
+      h_ctl_->sol += x.sol;
+      x.tree = x.sol = 0;
+    }
     const size_t c = dev_buf();
     if (c == 0) {
       h_ctl_->slot[0].nch = 0;

@@ -66,6 +66,12 @@ struct PoolCtl {
   // (workgroup steps, donations, idle waits, wall-clock ticks spent waiting)
   u64 pend_p[6];
   u64 pdiag[4];
+  // nodes pushed and leaves counted inside subtrees a thread explored to the end (N-Queens
+  // finishing: 64-bit counts, one accumulator line per 8th of the grid; the host folds them)
+  struct alignas(128) XAcc {
+    u64 tree, sol;
+    u64 pad[14];
+  } xacc[8];
   int perr;           // a persistent iteration's watchdog expired (nodes may be lost)
   int pad1;
   CtlI32 best;      // incumbent (atomicMin by leaves)
@@ -222,6 +228,7 @@ struct IterView {
   int cap;            // local DFS: no further step once the stack holds more than this
   int srank, sworld;
   bool persist;       // persistent iteration: work-sharing depth-first search in one kernel
+  bool armed;         // a rank split is pending: the pool is replicated on every rank
   unsigned pid;       // iteration number (Slot::pid)
 };
 
@@ -280,7 +287,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     // and leave — no table staging, no scans, no counter traffic
     v.C = v.B = v.nb = v.ns = v.L = v.Snew = v.bot = 0;
     v.nchunks = 0;
-    v.overflow = v.split = v.fused = v.local = v.persist = false;
+    v.overflow = v.split = v.fused = v.local = v.persist = v.armed = false;
     v.bp = BP;
     v.steps = v.cap = 0;
     v.srank = v.sworld = 0;
@@ -298,6 +305,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   v.C = static_cast<u64>(__builtin_amdgcn_readfirstlane(build_prefix(pa.cnt[b_in], v.nch_in, ps)));
   v.B = min(v.S + v.C, static_cast<u64>(pa.max_parents));
   const bool armed = v.sworld > 1 && !done_in && v.B > 0;
+  v.armed = armed;
   // Local DFS when the pool holds a backlog of pa.local_min parents (default: four
   // grid-filling windows of BP-parent chunks), never while the pool is replicated
   // (the split must see every level). Below that, breadth (one level per kernel,

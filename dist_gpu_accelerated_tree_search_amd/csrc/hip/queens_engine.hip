@@ -1,4 +1,7 @@
 // N-Queens device engine (traits + factory) and reference-style label evaluation.
+#include <algorithm>
+#include <cstdlib>
+
 #include "queens_engine.hpp"
 #include "queens_kernels.hpp"
 
@@ -41,6 +44,11 @@ static dev::QueensArgs queens_args(int N, int G) {
   a.N = N;
   a.G = G;
   a.full = N == 32 ? 0xffffffffu : ((1u << N) - 1u);
+  // subtree finishing: parents with at most finish_k columns left (TTS_QUEENS_FINISH
+  // overrides; 0 = level-by-level to the bottom)
+  a.finish_k = 7;
+  if (const char* f = std::getenv("TTS_QUEENS_FINISH")) a.finish_k = std::atoi(f);
+  a.finish_k = std::max(0, std::min(a.finish_k, dev::kQueensFinishMax));
   return a;
 }
 

@@ -16,6 +16,8 @@
 //            pool (pool_device.hpp, no device atomics).
 #pragma once
 
+#include <climits>
+
 #include "../core/pfsp_node.hpp"
 #include "pool_device.hpp"
 
@@ -27,11 +29,14 @@ struct QueensArgs {
   int N;
   int G;
   uint32_t full;
+  int finish_k;  // parents with at most this many columns left are explored to the end by their thread (0: off)
   // labels kernel only (reference-style evaluation, tests)
   const QueensNode* parents_in;
   uint8_t* labels_out;
   int nparents;
 };
+
+constexpr int kQueensFinishMax = 9;  // columns left at most in a finished subtree
 
 struct QueensSmem {
   static constexpr int BP = kBlock;
@@ -43,6 +48,7 @@ struct QueensSmem {
   uint8_t map[MAXCH];
   int scan[kBlock / kWave];
   int red[kBlock / kWave];
+  u64 fin[kBlock / kWave][2];
   PoolSmem<MAXCHUNKS> pool;
 };
 
@@ -72,6 +78,37 @@ __device__ inline uint32_t queens_free_rows(const QueensNode& nd, uint32_t full,
   return ok;
 }
 
+// Subtree finishing. Near the bottom of the tree a node's whole subtree is small and
+// generating it level by level through the device pool costs two 16-B global accesses per
+// node; instead the parent's thread walks it depth-first with every level's masks in
+// registers (template recursion = nested loops, no indexed stack) and counts with the
+// pool's rules: every safe child is a pushed node (tree), a child in the last column is
+// a complete board (sol) — the same tree as level-by-level expansion, -g work included.
+// A flat loop with the levels' untried rows in LDS (every lane advancing on its own,
+// no union of the lanes' trees) was measured 2x slower on N = 16 / 17
+// (profiles/r2/queens/README.md): the register walk's passes are cheap enough that
+// its divergence costs less than the flat loop's LDS round trips and branches.
+template <int L>
+__device__ inline void queens_dfs(uint32_t cols, uint32_t diag, uint32_t anti, int depth, const QueensArgs& a,
+                                  u64& tree, u64& sol) {
+  const QueensNode nd{cols, diag, anti, static_cast<uint32_t>(depth)};
+  uint32_t av = queens_free_rows(nd, a.full, a.G);
+  if (depth + 1 == a.N) {
+    const int c = __popc(av);
+    tree += static_cast<u64>(c);
+    sol += static_cast<u64>(c);
+    return;
+  }
+  if constexpr (L + 1 < kQueensFinishMax) {
+    tree += static_cast<u64>(__popc(av));
+    while (av) {
+      const uint32_t bit = av & (0u - av);
+      av ^= bit;
+      queens_dfs<L + 1>(cols | bit, (diag | bit) << 1, (anti | bit) >> 1, depth + 1, a, tree, sol);
+    }
+  }
+}
+
 // Position of the r-th (0-based) set bit of x (r < popcount(x)).
 __device__ inline int nth_set_bit(uint32_t x, int r) {
   int pos = 0;
@@ -99,6 +136,9 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
   pool_spill_leftovers<QueensNode, S::MAXCH, S::MAXCHUNKS>(pa, v, t, sm.pool);
 
+  // finishing (not while the pool is replicated across ranks: the split must see it)
+  const int fin_from = (a.finish_k > 0 && !v.armed) ? a.N - a.finish_k : INT_MAX;
+  u64 ftree = 0, fsol = 0;
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 gi = static_cast<u64>(ch) * S::BP + tid;
     int nchild = 0, leaf = 0;
@@ -108,6 +148,8 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
       if (static_cast<int>(nd.depth) == a.N) {
         // a leaf parent of the split iteration is replicated on every rank: rank 0 counts it
         leaf = (!v.split || v.srank == 0) ? 1 : 0;
+      } else if (static_cast<int>(nd.depth) >= fin_from) {
+        queens_dfs<0>(nd.cols, nd.diag, nd.anti, static_cast<int>(nd.depth), a, ftree, fsol);
       } else {
         uint32_t av = queens_free_rows(nd, a.full, a.G);
         if (v.split) {
@@ -137,6 +179,30 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
       dst[c] = QueensNode{nd.cols | bit, (nd.diag | bit) << 1, (nd.anti | bit) >> 1, nd.depth + 1};
     }
     __syncthreads();
+  }
+  if (fin_from != INT_MAX) {
+    // one pair of 64-bit adds per workgroup, on the line of its 8th of the grid
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      ftree += __shfl_xor(ftree, o, kWave);
+      fsol += __shfl_xor(fsol, o, kWave);
+    }
+    if ((tid & (kWave - 1)) == 0) {
+      sm.fin[tid / kWave][0] = ftree;
+      sm.fin[tid / kWave][1] = fsol;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < kBlock / kWave; ++w) {
+        ftree += sm.fin[w][0];
+        fsol += sm.fin[w][1];
+      }
+      if (ftree | fsol) {
+        auto& x = pa.ctl->xacc[blockIdx.x & 7];
+        __hip_atomic_fetch_add(&x.tree, ftree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&x.sol, fsol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 

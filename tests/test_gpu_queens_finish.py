@@ -1,0 +1,49 @@
+"""N-Queens subtree finishing (csrc/hip/queens_kernels.hpp queens_dfs): parents with at
+most TTS_QUEENS_FINISH columns left are explored to the end by their own thread. Every
+finishing depth must give the level-by-level tree and solution counts."""
+import pytest
+
+from dist_gpu_accelerated_tree_search_amd import EngineOptions, QueensModel, solve_engine
+
+pytestmark = pytest.mark.gpu
+
+GOLD = {8: (2056, 92), 10: (35538, 724), 12: (856188, 14200), 14: (27358552, 365596)}
+OPTS = EngineOptions(max_parents=1 << 20, ring_bytes=1 << 30)
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 5, 7, 9, 20])
+def test_finishing_depths_keep_the_tree(k, monkeypatch):
+    monkeypatch.setenv("TTS_QUEENS_FINISH", str(k))  # 20: clamped to the deepest template (9)
+    for N, gold in GOLD.items():
+        m = QueensModel(N)
+        eng = m.make_engine("gpu", 0, OPTS)
+        for _ in range(2):
+            r = solve_engine(m, eng)
+            assert (r.tree, r.sol) == gold, (N, k)
+        del eng
+
+
+def test_finishing_keeps_the_g_work_semantics(monkeypatch):
+    # -g 3: every candidate still tested 3 x depth times inside the finished subtrees; same tree
+    monkeypatch.setenv("TTS_QUEENS_FINISH", "7")
+    r = solve_engine(QueensModel(10, 3), QueensModel(10, 3).make_engine("gpu", 0, OPTS))
+    assert (r.tree, r.sol) == GOLD[10]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_finishing_after_in_search_split(world, monkeypatch):
+    # no finishing while the pool is replicated across ranks; the shares add up
+    monkeypatch.setenv("TTS_QUEENS_FINISH", "7")
+    m = QueensModel(12)
+    nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
+    tree = sol = 0
+    for r in range(world):
+        e = m.make_engine("gpu", 0, OPTS)
+        e.set_split(r, world, 2048)
+        e.begin(nodes, best)
+        e.run()
+        st = e.stats()
+        tree += st["tree"]
+        sol += st["sol"]
+        del e
+    assert (tree + tree1, sol + sol1) == GOLD[12]
