@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
         // a leaf parent of the split iteration is replicated on every rank: rank 0 counts it
         leaf = (!v.split || v.srank == 0) ? 1 : 0;
       } else if (static_cast<int>(nd.depth) >= fin_from) {
-        queens_dfs<0>(nd.cols, nd.diag, nd.anti, static_cast<int>(nd.depth), a, ftree, fsol);
+        // finished after the chunk loop, outside its barriers (no child, no leaf here)
       } else {
         uint32_t av = queens_free_rows(nd, a.full, a.G);
         if (v.split) {
@@ -181,6 +181,16 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
     __syncthreads();
   }
   if (fin_from != INT_MAX) {
+    // the subtrees of this workgroup's finishing parents (read again from the window):
+    // no barrier between them, so a wave with a deep subtree holds up no other wave
+    for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+      const u64 gi = static_cast<u64>(ch) * S::BP + tid;
+      if (gi < v.B) {
+        const QueensNode nd = *pool_parent<QueensNode, S::MAXCH, S::MAXCHUNKS>(pa, v, t, gi, sm.pool);
+        const int d = static_cast<int>(nd.depth);
+        if (d < a.N && d >= fin_from) queens_dfs<0>(nd.cols, nd.diag, nd.anti, d, a, ftree, fsol);
+      }
+    }
     // one pair of 64-bit adds per workgroup, on the line of its 8th of the grid
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {

@@ -19,7 +19,7 @@ for spec in "$@"; do
         -- python3 scripts/profile_workload.py "$wl" > "$out/$tag/p$pass.log" 2>&1 ) \
       || { echo "pass $pass of $tag failed"; tail -5 "$out/$tag/p$pass.log"; exit 1; }
   done
-  python3 scripts/pmc_summary.py "$out/$tag" pfsp_expand > "$out/$tag/summary.txt"
+  python3 scripts/pmc_summary.py "$out/$tag" "${KFILTER:-pfsp_expand}" > "$out/$tag/summary.txt"
   for pass in 1 2; do  # keep the per-kernel stats, drop the raw traces (gpurun_out must stay small)
     find "$out/$tag/p$pass" -name "*kernel_stats.csv" -exec cp {} "$out/$tag/p${pass}_kernel_stats.csv" \; 2>/dev/null
     rm -rf "$out/$tag/p$pass"
