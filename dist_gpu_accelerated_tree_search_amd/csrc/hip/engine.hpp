@@ -19,6 +19,8 @@
 #pragma once
 
 #include <algorithm>
+#include <array>
+#include <map>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -146,8 +148,10 @@ class DeviceEngine final : public IEngine {
       std::sort(ks_.begin(), ks_.end());
     }
     if (cfg_.use_graphs)
-      for (int k : ks_)
-        for (int m = 0; m < 2; ++m) graphs_[m].push_back(capture(k, m));
+      for (int ph = 0; ph < 2; ++ph)
+        for (int k : ks_)
+          for (int m = 0; m < 2; ++m) graphs_[ph][m].push_back(capture(k, m, 3 * ph));
+    if (const char* f = std::getenv("TTS_LEARN_FIRST")) learn_first_ = std::atoi(f) != 0;
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
     stats_.t_malloc = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -157,8 +161,11 @@ class DeviceEngine final : public IEngine {
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (xfer_) (void)hipStreamSynchronize(xfer_);
     spill_.clear();
-    for (auto& gs : graphs_)
-      for (auto g : gs) (void)hipGraphExecDestroy(g);
+    for (auto& gp : graphs_)
+      for (auto& gs : gp)
+        for (auto g : gs) (void)hipGraphExecDestroy(g);
+    for (auto& kv : first_graphs_)
+      for (auto g : kv.second) (void)hipGraphExecDestroy(g);
     for (void* p : owned_) (void)hipFree(p);
     (void)hipFree(d_ring_);
     for (int b = 0; b < 2; ++b) {
@@ -312,7 +319,13 @@ class DeviceEngine final : public IEngine {
       poll_transfers();
       size_t total = dev_total();
       const size_t all = total + spill_.size() + refill_n_;
-      if (all == 0) break;
+      if (all == 0) {
+        // the tree is done: the next solve's first replay gets this solve's iteration
+        // count (rounded up to whole phases), so it ends without empty iterations
+        const dev::u64 it = h_ctl_->iters;
+        learned_k_ = (it >= 3 && it <= 48) ? static_cast<int>((it + 2) / 3 * 3) : 0;
+        break;
+      }
       if (all < stop_below) break;
       if (max_launches >= 0 && launches >= max_launches) break;
       if (max_seconds > 0 && elapsed() >= max_seconds) break;
@@ -336,6 +349,11 @@ class DeviceEngine final : public IEngine {
         continue;
       }
       int gi = pick_graph(total, 0);
+      // right after begin(): as many iterations as the previous solve took, when known
+      const int kf = (fresh_ && learn_first_ && learned_k_ > 0 &&
+                      total + reserved_ + static_cast<size_t>(learned_k_ + 1) * buf_nodes_ <= cap_)
+                         ? learned_k_
+                         : 0;
       if (gi < 0) {
         if (!resv_.empty()) {  // ring span still being copied out: wait for the oldest copy
           TTS_HIP_CHECK(hipEventSynchronize(resv_.front().first));
@@ -350,7 +368,7 @@ class DeviceEngine final : public IEngine {
         upload_ctl();
         continue;
       }
-      launch_graph(gi);
+      launch_graph(gi, kf);
       ++launches;
       start_spill_ahead();
       // ---- pipelined replays: while one graph runs, queue the next one if the
@@ -358,7 +376,7 @@ class DeviceEngine final : public IEngine {
       // growth of both fits; then read the older graph's mirror. Hides the host
       // sync + launch gap between replays. ----
       size_t known = total;
-      size_t inflight_growth = static_cast<size_t>(ks_[gi] + 1) * buf_nodes_;
+      size_t inflight_growth = static_cast<size_t>((kf ? kf : ks_[gi]) + 1) * buf_nodes_;
       while (!inflight_.empty()) {
         const bool budget_ok = (max_launches < 0 || launches < max_launches) && (max_seconds <= 0 || elapsed() < max_seconds);
         if (inflight_.size() == 1 && budget_ok && known >= spec_min_) {
@@ -372,7 +390,7 @@ class DeviceEngine final : public IEngine {
         wait_oldest();
         check_overflow();
         known = dev_total();
-        inflight_growth = inflight_.empty() ? 0 : static_cast<size_t>(ks_[inflight_k_.front()] + 1) * buf_nodes_;
+        inflight_growth = inflight_.empty() ? 0 : static_cast<size_t>(inflight_k_.front() + 1) * buf_nodes_;
       }
     }
     stats_.t_run += elapsed();
@@ -439,6 +457,10 @@ class DeviceEngine final : public IEngine {
     // 6-iteration passes with a narrower parent window (plain launches: the
     // window is a kernel argument); identical on every rank
     const size_t win = std::max<size_t>(1, std::min(window, cfg_.max_parents));
+    if (phase_) {  // the passes below start from phase 0
+      normalize();
+      upload_ctl();
+    }
     for (int p = 0; p < passes; ++p) {
       if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
       const size_t total = dev_total();
@@ -451,10 +473,10 @@ class DeviceEngine final : public IEngine {
       next_mirror_ ^= 1;
       for (int i = 0; i < 6; ++i) Traits::launch(a, i, grid_, stream_);
       a.pool.mirror = d_mirror_[m];
-      Traits::finalize(a.pool, stream_);
+      Traits::finalize(a.pool, 0, stream_);
       TTS_HIP_CHECK(hipGetLastError());
       TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
-      push_inflight(m, 0);
+      push_inflight(m, 6);
       ++stats_.launches;
       sync_ctl();
     }
@@ -635,8 +657,8 @@ class DeviceEngine final : public IEngine {
     TTS_HIP_CHECK(hipEventRecord(up_done_, stream_));
   }
 
-  // Host shadow must be current (sync_ctl) and state slot 0 / buffer 0 active,
-  // which holds between graph replays (K is a multiple of 6).
+  // Host shadow must be current (sync_ctl); between graph replays slot 0 is active
+  // and the latest children are in buffer phase_ & 1 (graphs of 3k iterations).
   void normalize() {
     // counts of a persistent last iteration join the plain counters (the next
     // iteration must not fold them again)
@@ -655,6 +677,7 @@ class DeviceEngine final : public IEngine {
     }
     const size_t c = dev_buf();
     if (c == 0) {
+      phase_ = 0;
       h_ctl_->slot[0].nch = 0;
       h_ctl_->sol += h_ctl_->pend_leaves;
       h_ctl_->tree += h_ctl_->pend_internal;
@@ -663,13 +686,14 @@ class DeviceEngine final : public IEngine {
     }
     if (dev_stack() + c > cap_) throw std::runtime_error("device ring capacity exceeded");
     // the flatten kernel reads the device ctl, which equals the host shadow here
-    Traits::flatten(args_.pool, grid_, stream_);
+    Traits::flatten(args_.pool, phase_ & 1, grid_, stream_);
     TTS_HIP_CHECK(hipGetLastError());
     h_ctl_->slot[0].stack += c;
     h_ctl_->tree += c + h_ctl_->pend_internal;
     h_ctl_->sol += h_ctl_->pend_leaves;
     h_ctl_->slot[0].nch = 0;
     h_ctl_->pend_children = h_ctl_->pend_leaves = h_ctl_->pend_internal = 0;
+    phase_ = 0;  // no buffered children: the next iteration may read either buffer
   }
 
   void ring_write_top(const Node* src, size_t n, hipMemcpyKind kind) {
@@ -880,38 +904,55 @@ class DeviceEngine final : public IEngine {
     upload_ctl();
   }
 
-  void launch_graph(int gi) {
+  // Graphs hold 3k iterations, so a replay starts and ends at phase 0 or 3 (iteration t
+  // reads slot t % 3 — slot 0 at both — and buffer t & 1): phase_ is the next
+  // iteration's t, and every graph exists for both start phases. K < 0: the learned
+  // first-replay graph of -K iterations (learn_first_).
+  void launch_graph(int gi, int K = 0) {
     const int m = next_mirror_;
     next_mirror_ ^= 1;
+    const int k = K > 0 ? K : ks_[gi];
     if (cfg_.use_graphs) {
-      TTS_HIP_CHECK(hipGraphLaunch(graphs_[m][gi], stream_));
+      hipGraphExec_t g = K > 0 ? first_graph(K)[m] : graphs_[phase_ / 3][m][gi];
+      TTS_HIP_CHECK(hipGraphLaunch(g, stream_));
     } else {
-      for (int i = 0; i < ks_[gi]; ++i) launch_iter(args_, i % 6, stream_);
+      for (int i = 0; i < k; ++i) launch_iter(args_, (phase_ + i) % 6, stream_);
       auto pa = args_.pool;
       pa.mirror = d_mirror_[m];
-      Traits::finalize(pa, stream_);
+      Traits::finalize(pa, ((phase_ + k) % 6) & 1, stream_);
       TTS_HIP_CHECK(hipGetLastError());
     }
     TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
-    push_inflight(m, gi);
+    push_inflight(m, k);
+    phase_ = (phase_ + k) % 6;
     ++stats_.launches;
     fresh_ = false;
   }
-  void push_inflight(int m, int gi) {
+  // The learned first replay (phase 0, both mirrors), captured on first use.
+  const std::array<hipGraphExec_t, 2>& first_graph(int K) {
+    auto it = first_graphs_.find(K);
+    if (it == first_graphs_.end()) {
+      TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+      std::array<hipGraphExec_t, 2> g{capture(K, 0, 0), capture(K, 1, 0)};
+      it = first_graphs_.emplace(K, g).first;
+    }
+    return it->second;
+  }
+  void push_inflight(int m, int k) {
     inflight_.push_back(m);
-    inflight_k_.push_back(gi);
+    inflight_k_.push_back(k);  // iterations of the replay
     inflight_seq_.push_back(++launched_seq_);
   }
 
-  hipGraphExec_t capture(int K, int mirror) {
+  hipGraphExec_t capture(int K, int mirror, int phase) {
     hipStream_t cs;
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     hipGraph_t g;
     TTS_HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < K; ++i) launch_iter(args_, i % 6, cs);
+    for (int i = 0; i < K; ++i) launch_iter(args_, (phase + i) % 6, cs);
     auto pa = args_.pool;
     pa.mirror = d_mirror_[mirror];
-    Traits::finalize(pa, cs);
+    Traits::finalize(pa, ((phase + K) % 6) & 1, cs);
     TTS_HIP_CHECK(hipStreamEndCapture(cs, &g));
     hipGraphExec_t exec;
     TTS_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
@@ -961,7 +1002,11 @@ class DeviceEngine final : public IEngine {
   size_t arm_min_ = 1;
   hipStream_t stream_ = nullptr, own_stream_ = nullptr;
   std::vector<int> ks_;
-  std::vector<hipGraphExec_t> graphs_[2];
+  std::vector<hipGraphExec_t> graphs_[2][2];  // [start phase 0 / 3][mirror][graph]
+  std::map<int, std::array<hipGraphExec_t, 2>> first_graphs_;  // learned first replays by length
+  int phase_ = 0;         // t of the next iteration: 0 or 3
+  bool learn_first_ = true;  // first replay after begin() = the previous solve's iterations (TTS_LEARN_FIRST=0: off)
+  int learned_k_ = 0;     // ... rounded up to 3k (0: unknown)
   std::vector<void*> owned_;
   PinnedSpill<Node> spill_;
   EngineStats stats_;

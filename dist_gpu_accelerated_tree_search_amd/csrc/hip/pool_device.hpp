@@ -429,17 +429,18 @@ __device__ inline void pool_spill_leftovers(const PoolArgs<Node>& pa, const Iter
 
 // Host-requested: move the whole buffer (slot 0 / buffer 0, i.e. between graph
 // replays) onto the ring top. The host then folds the counts into ctl.
+// (b: the buffer the latest iteration wrote; graphs end at phase 0 or 3, slot 0 either way)
 template <class Node, int MAXCH, int MAXCHUNKS>
-__global__ __launch_bounds__(kBlock) void pool_flatten_kernel(PoolArgs<Node> pa) {
+__global__ __launch_bounds__(kBlock) void pool_flatten_kernel(PoolArgs<Node> pa, int b) {
   __shared__ PoolSmem<MAXCHUNKS> ps;
   IterView v;
   v.S = pa.ctl->slot[0].stack;
   v.bot = pa.ctl->bot;
   v.nch_in = pa.ctl->slot[0].nch;
-  v.C = static_cast<u64>(build_prefix(pa.cnt[0], v.nch_in, ps));
+  v.C = static_cast<u64>(build_prefix(pa.cnt[b], v.nch_in, ps));
   v.nb = 0;
   v.L = v.C;
-  pool_spill_leftovers<Node, MAXCH, MAXCHUNKS>(pa, v, 0, ps);
+  pool_spill_leftovers<Node, MAXCH, MAXCHUNKS>(pa, v, b, ps);
 }
 
 // Rank share of a replicated pool: out[t] = ring[bot + rank + t*world], t < keep
@@ -485,15 +486,18 @@ __global__ __launch_bounds__(kBlock) void pool_weight_kernel(const Node* __restr
 // The control block is published to host-mapped memory with system-scope stores,
 // the sequence number last (release): the host polls that word instead of
 // waiting for the graph's completion signal (engine.hpp wait_oldest).
+// (b: the buffer the graph's last iteration wrote — graphs of 3k iterations end at phase 0
+// or 3: slot 0 either way, buffer b = phase & 1; that iteration's persistent records are
+// pst[b ^ 1])
 template <class Node, int MAXCHUNKS>
-__global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa) {
+__global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa, int b) {
   __shared__ PoolSmem<MAXCHUNKS> ps;
   const int n = pa.ctl->slot[0].nch;
   const u64 seq = pa.ctl->seq + 1;
   int c = 0, l = 0, in = 0;
   for (int i = threadIdx.x; i < n; i += kBlock) {
-    c += pa.cnt[0][i];
-    const int x = pa.lcnt[0][i];
+    c += pa.cnt[b][i];
+    const int x = pa.lcnt[b][i];
     l += lcnt_leaves(x);
     in += lcnt_inner(x);
   }
@@ -501,9 +505,9 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   (void)block_exclusive_scan(c, ps.scan, &ct);
   (void)block_exclusive_scan(l, ps.red, &lt);
   (void)block_exclusive_scan(in, ps.scan, &it);
-  // the graph's last iteration (t = 5, parity 1) was persistent: its counts
+  // the graph's last iteration was persistent: its counts
   u64 pc[6] = {0, 0, 0, 0, 0, 0};
-  if (pa.ctl->slot[0].pers) persist_sum<Node, MAXCHUNKS>(pa, 1, ps, pc);
+  if (pa.ctl->slot[0].pers) persist_sum<Node, MAXCHUNKS>(pa, b ^ 1, ps, pc);
   if (threadIdx.x == 0) {
     pa.ctl->pend_children = static_cast<u64>(ct);
     pa.ctl->pend_leaves = static_cast<u64>(lt);

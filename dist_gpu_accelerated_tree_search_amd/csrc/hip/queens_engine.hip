@@ -20,12 +20,12 @@ struct QueensTraits {
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL(dev::queens_expand_kernel, dim3(grid), dim3(dev::kBlock), 0, s, a, t);
   }
-  static void flatten(const dev::PoolArgs<Node>& pa, int grid, hipStream_t s) {
+  static void flatten(const dev::PoolArgs<Node>& pa, int b, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, S::MAXCH, S::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
-                       pa);
+                       pa, b);
   }
-  static void finalize(const dev::PoolArgs<Node>& pa, hipStream_t s) {
-    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, S::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa);
+  static void finalize(const dev::PoolArgs<Node>& pa, int b, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, S::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa, b);
   }
   static int blocks_per_cu() {
     int n = 0;

@@ -239,3 +239,18 @@ def test_lb1_iteration_modes(monkeypatch, env):
     eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=1 << 20, iters_large=12))
     r = solve_engine(model, eng)
     assert (r.tree, r.sol, r.best) == GOLDEN[(14, 1)]
+
+
+def test_learned_first_replay_then_longer_tree():
+    # the first replay after begin() has as many iterations as the previous solve (15 for
+    # ta014 -u 1, a graph ending at phase 3); a longer search then continues with the
+    # phase-3 graphs, through spills on a small ring, and must still give exact counts
+    m = PfspModel(14, 1)
+    eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 16, ring_bytes=1 << 24))
+    for _ in range(2):
+        r = solve_engine(m, eng, ub=1)
+        assert (r.tree, r.sol, r.best) == GOLDEN[(14, 1)]
+    r0 = solve_engine(m, eng, ub=0)  # no incumbent: a larger tree, the optimum found
+    assert r0.best == 1377 and r0.tree > GOLDEN[(14, 1)][0]
+    r = solve_engine(m, eng, ub=1)
+    assert (r.tree, r.sol, r.best) == GOLDEN[(14, 1)]
