@@ -124,9 +124,9 @@ struct PoolArgs {
   // holds at least persist_min parents, persist_wg workgroups each run a depth-first
   // search on a private stack (persist_r chunk slots) until the whole window's subtrees
   // are explored or persist_ticks wall-clock ticks have passed, sharing work in the kernel:
-  // an idle workgroup posts an odd generation in want[wg]; a donor claims it (CAS to
+  // an idle workgroup posts an odd generation in box[wg].want; a donor claims it (CAS to
   // even), copies the bottom half of its own stack into the receiver's slots and
-  // publishes {generation, count} in mail[wg] (agent release / acquire).
+  // publishes {generation, count} in box[wg].mail (write-through payload, agent acquire).
   u64 persist_min;  // 0: off
   u64 persist_ticks;  // budget in wall-clock ticks (s_memrealtime)
   int persist_wg;
