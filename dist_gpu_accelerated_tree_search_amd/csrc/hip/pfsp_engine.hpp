@@ -175,6 +175,10 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
   a.npairs = PR;
   a.rs4 = img.rs4;
   a.lb2_pipe = lb2_pipe_wanted();
+  // last-level finishing: ta008 LB1_d 5.62 -> 5.45 ms, ta014 LB1 0.296 -> 0.30 ms
+  // (profiles/r2/lb1_fin.txt): off by default, TTS_LB1_FIN=1 turns it on
+  a.lb1_fin = 0;
+  if (const char* f = std::getenv("TTS_LB1_FIN")) a.lb1_fin = std::atoi(f) != 0;
   a.lb2_dyn = lb2_dyn_wanted();
   a.lb2_stride = lb2_stride_wanted();
   for (int m = 0; m < M; ++m) {

@@ -121,6 +121,9 @@ struct PfspArgs {
   // per-workgroup timeline (probe only): wall clock (s_memrealtime) at entry, after
   // the iteration prologue, and at exit, 3 values per workgroup
   unsigned long long* dbg_blk;
+  // one-level LB1 loop: parents with two jobs left evaluate their children's complete
+  // schedules in place (lb1_small_parent FIN; TTS_LB1_FIN=1: on)
+  int lb1_fin;
 };
 
 template <int NJ, int M, int LBK>
@@ -1289,9 +1292,18 @@ struct PfspSmemLB1s {
 
 // Bounds of every child of the parent held in w (valid lanes only); calls
 // emit(k, lb) for each child position k (static after unrolling).
-template <int NJ, int M, class Emit>
+//
+// FIN (the one-level loop, a.lb1_fin): a parent with two jobs left hands its children to
+// fin(k, lb, leaf_lb) instead: the child's bound and the bound of its single child, the
+// complete schedule (what the next iteration would compute with the child as parent), so
+// the last tree level never goes through the pool.
+struct NoFin {
+  __device__ void operator()(int, int, int) const {}
+};
+template <int NJ, int M, bool FIN = false, class Emit, class Fin = NoFin>
 __device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const PfspSmemLB1s<NJ, M>& sm,
-                                        const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], Emit emit) {
+                                        const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], Emit emit,
+                                        Fin fin = Fin{}) {
   const auto& ptab = sm.ptab;
   const int d = static_cast<int>(w[0] & 0xffu);
   // r[m] = unscheduled work on machine m + its min tail: the tail is folded in
@@ -1317,9 +1329,10 @@ __device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const PfspSmem
       }
     }
   }
+  const bool pre = FIN && a.lb1_fin && d + 2 == a.jobs;
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
-    if (k >= d && k < a.jobs) {
+    if (k >= d && k < a.jobs && !pre) {
       const int job = static_cast<int>((w[(1 + k) >> 2] >> (((1 + k) & 3) * 8)) & 0xffu);
       int pr[M];
       load_prow<M>(ptab[job], pr);
@@ -1332,6 +1345,38 @@ __device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const PfspSmem
         tt = sv + pr[m];
       }
       emit(k, lb);
+    }
+  }
+  if constexpr (FIN) {
+    if (pre) {
+#pragma unroll 1
+      for (int q = 0; q < 2; ++q) {
+        const int k = d + q, o = d + 1 - q;  // the child's job position and the last job's
+        const int jk = static_cast<int>(node_byte<NJ>(w, 1 + k)), jo = static_cast<int>(node_byte<NJ>(w, 1 + o));
+        int pk[M], po[M], fc[M];
+        load_prow<M>(ptab[jk], pk);
+        load_prow<M>(ptab[jo], po);
+        int lb = f[0] + r[0];
+        int tt = f[0] + pk[0];
+        fc[0] = tt;
+#pragma unroll
+        for (int m = 1; m < M; ++m) {
+          const int sv = max(tt, f[m]);
+          lb = max(lb, sv + r[m]);
+          tt = sv + pk[m];
+          fc[m] = tt;
+        }
+        // the complete schedule: the child as parent (remain r - pk), the last job
+        int lbl = fc[0] + r[0] - pk[0];
+        int t2 = fc[0] + po[0];
+#pragma unroll
+        for (int m = 1; m < M; ++m) {
+          const int sv = max(t2, fc[m]);
+          lbl = max(lbl, sv + r[m] - pk[m]);
+          t2 = sv + po[m];
+        }
+        fin(k, lb, lbl);
+      }
     }
   }
 }
@@ -1947,24 +1992,39 @@ __device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
 #pragma unroll 1
       for (int k = 0; k < NJ; ++k) kmask |= split_keep(v, gi, k) ? (1u << k) : 0u;
     }
+    int ninner = 0;
     if (valid) {
-      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
-        const bool keep = (kmask >> k) & 1u;
-        if (leaf) {
-          nleaf += keep;
-          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-        } else if (keep && lb < best) {
-          ++nsurv;
-          surv |= 1u << k;
-        }
-      });
+      lb1_small_parent<NJ, M, true>(
+          a, sm, w,
+          [&](int k, int lb) {
+            const bool keep = (kmask >> k) & 1u;
+            if (leaf) {
+              nleaf += keep;
+              if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+            } else if (keep && lb < best) {
+              ++nsurv;
+              surv |= 1u << k;
+            }
+          },
+          [&](int k, int lb, int lbl) {  // a child with one job left: explored here
+            if (((kmask >> k) & 1u) && lb < best) {
+              ++ninner;  // the child, pushed and expanded; its leaf counts as one more leaf
+              if (lbl < best) atomicMin(&pa.ctl->best.v, lbl);
+            }
+          });
     }
-    // one scan for both counts: survivors in the low 16 bits, leaves in the high
+    // one scan for all counts, fields that cannot carry into each other: survivors
+    // (<= 256 x 19) in bits 0-12, leaf parents' leaves (<= 256) in 13-21, children
+    // explored in place (<= 512, one leaf each) in 22-31
     int tot = 0;
-    const int off = block_exclusive_scan(nsurv | (nleaf << 16), sm.scan, &tot) & 0xffff;
+    const uint32_t packed = static_cast<uint32_t>(nsurv) | (static_cast<uint32_t>(nleaf) << 13) |
+                            (static_cast<uint32_t>(ninner) << 22);
+    const int off = block_exclusive_scan(static_cast<int>(packed), sm.scan, &tot) & 0x1fff;
     if (tid == 0) {
-      cnt_out[ch] = tot & 0xffff;
-      lcnt_out[ch] = tot >> 16;
+      const uint32_t u = static_cast<uint32_t>(tot);
+      const int inner = static_cast<int>(u >> 22);
+      cnt_out[ch] = static_cast<int>(u & 0x1fffu);
+      lcnt_out[ch] = (static_cast<int>((u >> 13) & 0x1ffu) + inner) | (inner << 16);
     }
     if (surv) {
       const uint32_t jd = node_byte<NJ>(w, 1 + d);
