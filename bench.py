@@ -8,6 +8,16 @@ i.e. STRONG scaling: the tree (2,573,652 nodes, sol 2,648, makespan 1377) is the
 same at every N. Each step's tree/sol/makespan is checked against the golden
 values, so a skipped or truncated search fails instead of reporting a number.
 
+After the timed headline loop the other BASELINE multi-GPU configs run in the same
+job (all ranks cooperating, same runtime), unless --no-extras:
+  * ta021 (20x20) LB1_d, one complete solve: makespan 2297 and the -u 1 tree
+    (260,069,628,524 nodes, sol 14,963,858 — deterministic at every N) are checked;
+  * ta056 (50x20) LB2, a fixed time box (--box-s, default 10 s): explored nodes/s
+    (the tree is ~4.6e19 nodes, profiles/r2/ta056_projection.md: no complete solve).
+They become fields of the same single JSON line ("extras"). An extra that fails is
+reported there (and on stderr) and the headline line is still printed; a watchdog
+(--extras-timeout) prints the line and ends every rank if an extra hangs.
+
 Launch: python bench.py [--gpus 1 --steps K --warmup W]
         python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
                --master-port P bench.py --gpus N --steps K --warmup W
@@ -19,6 +29,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 # ta014 LB1 (-u 1) golden values and the reference throughput on the same tree.
@@ -26,10 +37,32 @@ GOLDEN = {(14, 1): (2573652, 2648, 1377), (14, 0): (2573652, 2648, 1377), (14, 2
 # fastest reference implementation of this tree = pfsp_omp_c.out -C 8
 # -l 0 (LB1_d, identical tree to LB1) at 23 M nodes/s; no published GPU number exists.
 BASELINE_NODES_PER_S = 23.0e6
+# ta021 LB1_d -u 1: tree / sol / makespan measured on one MI355X (profiles/r2/suite/);
+# the makespan is Taillard's optimum. Reference single-GPU wall times (bound not
+# recorded, pfsp/data/single-GPU.py:23,42): V100 CUDA 1308.79 s, MI50 HIP 2538.23 s.
+TA021_GOLDEN = (260069628524, 14963858, 2297)
+TA021_REF_S = 1308.79
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+class Emitter:
+    """Prints the single JSON line exactly once (main thread or watchdog)."""
+
+    def __init__(self, rank: int):
+        self.rank = rank
+        self.lock = threading.Lock()
+        self.done = False
+
+    def emit(self, rec: dict) -> None:
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.rank == 0:
+                print(json.dumps(rec), flush=True)
 
 
 def main() -> int:
@@ -48,6 +81,14 @@ def main() -> int:
     ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
                     help="process group for node transfers (gloo: ranks may share one GPU, for tests)")
     ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default LOCAL_RANK)")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (no ta021 / ta056 runs)")
+    ap.add_argument("--extras", default="ta021,ta056", help="comma list of extras to run")
+    ap.add_argument("--box-s", type=float, default=10.0, help="ta056 LB2 time box (seconds)")
+    ap.add_argument("--extras-timeout", type=float, default=900.0,
+                    help="watchdog: print the line and end every rank after this many seconds of extras")
+    ap.add_argument("--extra-inst-lb1d", type=int, default=21, help=argparse.SUPPRESS)
+    ap.add_argument("--extra-inst-lb2", type=int, default=56, help=argparse.SUPPRESS)
+    ap.add_argument("--extra-ring-gb", type=float, default=64.0)
     a = ap.parse_args()
 
     import torch  # noqa: F401  (before the HIP extension: one HIP runtime per process)
@@ -60,6 +101,9 @@ def main() -> int:
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     comm = Comm(use_gpu=(a.backend == "gpu" and a.comm == "nccl"), device=a.device)
+    if comm.preflight is not None:
+        log(f"rank {comm.rank}: RCCL point-to-point preflight ok: {comm.preflight}")
+    out = Emitter(comm.rank)
     model = PfspModel(a.inst, a.lb)
     opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * (1 << 30)))
     device = (comm.topo.local_rank if a.device is None else a.device) if a.backend == "gpu" else 0
@@ -93,40 +137,115 @@ def main() -> int:
     dt = float(comm.allgather_f64([dt_local]).max())
     value = tree / dt
     if comm.rank == 0:
-        ex = last.extra
         log(f"last step: elapsed {last.elapsed * 1e3:.3f} ms, init {last.t_init * 1e3:.3f} ms, "
-            f"search {last.t_search * 1e3:.3f} ms, rounds {ex.get('rounds')}, "
+            f"search {last.t_search * 1e3:.3f} ms, rounds {last.extra.get('rounds')}, "
             f"per-rank tree {[w.tree for w in last.workers]}, control plane "
             f"{'shm' if getattr(comm, 'ctl', None) is not None else comm.backend}")
-        rec = {
-            "metric": "tree-nodes/sec (whole node), PFSP ta014 LB1 at 1/2/4/8 MI355X",
-            "value": value,
-            "unit": "nodes/s",
-            "n_gpus": comm.world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": dt / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": value / BASELINE_NODES_PER_S,
-            "dtype": "int32",
-            "data": "Taillard ta%03d regenerated from its seed (exact benchmark instance, no download)" % a.inst,
-            "config": {
-                "model": f"PFSP ta{a.inst:03d} ({model.jobs}x{model.machines}) {['LB1_d', 'LB1', 'LB2'][a.lb]} -u {a.ub}",
-                "global_batch": a.max_parents,
-                "seq_len": model.jobs,
-                "parallelism": f"dp{comm.world}" + ("" if a.no_ws else "+ws"),
-                "tree": last.tree,
-                "sol": last.sol,
-                "makespan": last.best,
-                "rounds_last_step": last.extra.get("rounds"),
-                "baseline": "reference pfsp_omp_c.out -C 8 -l 0, 23 M nodes/s (BASELINE.md, same tree)",
-            },
-        }
-        print(json.dumps(rec), flush=True)
-    del engine
+    rec = {
+        "metric": "tree-nodes/sec (whole node), PFSP ta014 LB1 at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "nodes/s",
+        "n_gpus": comm.world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": value / BASELINE_NODES_PER_S,
+        "dtype": "int32",
+        "data": "Taillard ta%03d regenerated from its seed (exact benchmark instance, no download)" % a.inst,
+        "config": {
+            "model": f"PFSP ta{a.inst:03d} ({model.jobs}x{model.machines}) {['LB1_d', 'LB1', 'LB2'][a.lb]} -u {a.ub}",
+            "global_batch": a.max_parents,
+            "seq_len": model.jobs,
+            "parallelism": f"dp{comm.world}" + ("" if a.no_ws else "+ws"),
+            "tree": last.tree,
+            "sol": last.sol,
+            "makespan": last.best,
+            "rounds_last_step": last.extra.get("rounds"),
+            "baseline": "reference pfsp_omp_c.out -C 8 -l 0, 23 M nodes/s (BASELINE.md, same tree)",
+            "p2p_preflight": comm.preflight,
+        },
+    }
+    del solver, engine
+
+    if not a.no_extras:
+        extras: dict = {}
+        rec["extras"] = extras
+
+        def fire():
+            extras["error"] = f"watchdog: extras exceeded {a.extras_timeout:.0f} s; every rank exits"
+            log(f"rank {comm.rank}: {extras['error']}")
+            out.emit(rec)
+            os._exit(0)
+
+        dog = threading.Timer(a.extras_timeout, fire)
+        dog.daemon = True
+        dog.start()
+        which = [x for x in a.extras.split(",") if x]
+        ok = True
+        for name in which:
+            if not ok:
+                extras[name] = {"skipped": "an earlier extra failed"}
+                continue
+            try:
+                if name == "ta021":
+                    extras[name] = run_solve_extra(a, comm, device, a.extra_inst_lb1d, 0, time_limit=0.0)
+                elif name == "ta056":
+                    extras[name] = run_solve_extra(a, comm, device, a.extra_inst_lb2, 2, time_limit=a.box_s)
+                else:
+                    extras[name] = {"error": "unknown extra"}
+                mine_ok = 1
+            except Exception as e:  # noqa: BLE001 - reported in the line, headline still printed
+                log(f"rank {comm.rank}: extra {name} failed: {e!r}")
+                extras[name] = {"error": repr(e)[:300]}
+                mine_ok = 0
+            # every rank learns whether all ranks succeeded before the next collective solve
+            ok = bool(comm.allreduce_i64([mine_ok], "min")[0])
+        dog.cancel()
+    out.emit(rec)
     comm.close()
     return 0
+
+
+def run_solve_extra(a, comm, device: int, inst: int, lb: int, time_limit: float) -> dict:
+    """One cooperative solve (or a time box) of another BASELINE config on all ranks,
+    with the headline's runtime (DistSolver: same Step 1, split and rounds)."""
+    from dist_gpu_accelerated_tree_search_amd.models.pfsp import EngineOptions, PfspModel
+    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig, DistSolver
+
+    model = PfspModel(inst, lb)
+    opts = EngineOptions(ring_bytes=int(a.extra_ring_gb * (1 << 30)))
+    t_setup = time.perf_counter()
+    engine = model.make_engine(a.backend, device, opts)
+    cfg = DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws, time_limit_s=time_limit)
+    solver = DistSolver(model, engine, comm, cfg, window=opts.max_parents)
+    t_setup = time.perf_counter() - t_setup
+    comm.barrier()
+    t0 = time.perf_counter()
+    raw = solver.solve_raw(1)
+    comm.barrier()
+    dt = float(comm.allgather_f64([time.perf_counter() - t0]).max())
+    r = solver.result(*raw)
+    name = f"ta{inst:03d} ({model.jobs}x{model.machines}) {['LB1_d', 'LB1', 'LB2'][lb]} -u 1"
+    d = {"config": name, "n_gpus": comm.world, "seconds": dt, "tree": r.tree, "sol": r.sol, "makespan": r.best,
+         "nodes_per_s": r.tree / dt, "complete": bool(r.extra.get("complete", True)),
+         "rounds": r.extra.get("rounds"), "per_rank_tree": [w.tree for w in r.workers],
+         "engine_setup_s": t_setup}
+    if time_limit > 0:
+        d["time_box_s"] = time_limit
+    else:
+        gold = TA021_GOLDEN if (inst, lb) == (21, 0) else None
+        if gold is not None:
+            d["golden_ok"] = (r.tree, r.sol, r.best) == gold
+            d["ref_seconds_v100"] = TA021_REF_S
+            d["speedup_vs_ref"] = TA021_REF_S / dt
+            if not d["golden_ok"]:
+                raise RuntimeError(f"{name}: (tree, sol, makespan) {(r.tree, r.sol, r.best)} != golden {gold}")
+        elif r.best != model.best_known:
+            raise RuntimeError(f"{name}: makespan {r.best} != best known {model.best_known}")
+    del solver, engine
+    return d
 
 
 if __name__ == "__main__":

@@ -184,6 +184,8 @@ inline DistOptions dist_options_from(const py::dict& o) {
   get("local_world", opt.local_world);
   get("early_rounds", opt.early_rounds);
   get("max_rounds", opt.max_rounds);
+  get("time_limit", opt.time_limit);
+  get("live_best", opt.live_best);
   get("checkpoint_every", opt.checkpoint_every);
   get("watchdog_s", opt.watchdog_s);
   get("watchdog_abort", opt.watchdog_abort);
@@ -272,6 +274,7 @@ struct PyDistSession {
   TransferFn xfer;
   RoundHook hook;
   size_t warm_target = 25, split_min = 1;
+  bool split = true;
   DistSolveResult last;
 };
 
@@ -312,8 +315,9 @@ inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory) {
   py::class_<PyDistSession>(m, "DistSession", py::module_local())
       .def(py::init([warmup_factory](py::object engine, py::object model, uintptr_t shm_address, py::object allgather_fn,
                                      int rank, int world, py::dict o, py::object transfer_fn, py::object round_hook,
-                                     size_t warm_target, size_t split_min, double timeout_s) {
+                                     size_t warm_target, size_t split_min, double timeout_s, bool split) {
              auto s = std::make_unique<PyDistSession>();
+             s->split = split;
              s->engine_ref = engine;
              s->e = engine.cast<IEngine*>();
              s->ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s);
@@ -327,13 +331,15 @@ inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory) {
            }),
            py::arg("engine"), py::arg("model"), py::arg("shm_address"), py::arg("allgather_fn"), py::arg("rank"),
            py::arg("world"), py::arg("options"), py::arg("transfer_fn"), py::arg("round_hook") = py::none(),
-           py::arg("warm_target") = 25, py::arg("split_min") = 1, py::arg("timeout_s") = 1800.0)
+           py::arg("warm_target") = 25, py::arg("split_min") = 1, py::arg("timeout_s") = 1800.0,
+           py::arg("split") = true)
       .def(
           "solve",
           [](PyDistSession& s, int best) {
             {
               py::gil_scoped_release nogil;
-              s.last = dist_solve_split(*s.e, *s.ctl, s.opt, s.warm, best, s.warm_target, s.split_min, s.xfer, s.hook);
+              s.last = dist_solve_split(*s.e, *s.ctl, s.opt, s.warm, best, s.warm_target, s.split_min, s.xfer, s.hook,
+                                        s.split);
             }
             const auto& r = s.last;
             return py::make_tuple(r.best, r.tree, r.sol, r.rounds, r.complete, r.t_init, r.t_search, r.elapsed);

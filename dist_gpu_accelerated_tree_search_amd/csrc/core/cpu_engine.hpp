@@ -70,7 +70,12 @@ class CpuEngine final : public IEngine {
     while (!pool_.empty() && pool_.size() >= std::max<size_t>(stop_below, 1)) {
       if (max_launches >= 0 && launches >= max_launches) break;
       if (max_seconds > 0 && now_s() - t0 >= max_seconds) break;
-      if (hook_ && hook_(pool_.size())) break;
+      if (hook_) {
+        int b = best_;
+        const bool stop = hook_(pool_.size(), b);
+        best_ = std::min(best_, b);
+        if (stop) break;
+      }
       const size_t n = pool_.pop_back_bulk_free(1, batch_, parents.data(), 1);
       expand(parents.data(), n);
       parents_ += n;

@@ -57,6 +57,10 @@ class RoundControl {
   virtual void request_next_round() {}
   virtual void request_current_round() {}
   virtual bool round_requested() const { return false; }
+  // live incumbent between rounds (board only): start of a cooperative solve, and
+  // offer `b` / get the best offered by any rank in this solve
+  virtual void begin_solve() {}
+  virtual int exchange_best(int b) { return b; }
 };
 
 class ShmRoundControl final : public RoundControl {
@@ -76,6 +80,8 @@ class ShmRoundControl final : public RoundControl {
   void request_next_round() override { c_->request_round(c_->rounds() + 1); }
   void request_current_round() override { c_->request_round(c_->rounds()); }
   bool round_requested() const override { return c_->round_requested(); }
+  void begin_solve() override { c_->begin_solve(); }
+  int exchange_best(int b) override { return c_->exchange_best(b); }
 
  private:
   ShmControl* c_;
@@ -153,6 +159,9 @@ struct DistOptions {
   int local_world = 0;                            // ranks per node (0: all on one node)
   bool early_rounds = true;                       // board-driven early rounds (shm control only)
   long max_rounds = 0;                            // stop after this many rounds in total (0: never)
+  double time_limit = 0;                          // stop at the first round after this many seconds
+                                                  // on any rank (0: never; throughput time boxes)
+  bool live_best = true;                          // exchange the incumbent after every replay (board)
   long checkpoint_every = 0;                      // RoundHook every k rounds (0: never)
   double watchdog_s = 0;                          // report a phase longer than this
   bool watchdog_abort = false;
@@ -234,9 +243,15 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     }
   } finish{finished, dog};
 
-  // ---- board hook: publish the live pool size; leave the slice on a peer's request ----
-  e.set_progress_hook([&](size_t pool) {
+  // ---- board hook, after every graph replay: publish the live pool size, exchange
+  // the incumbent with every rank (a better solution prunes everywhere at once, not
+  // at the next round: ref checkBest, pfsp_multigpu_cuda.c:30-50,307-312), and leave
+  // the slice on a peer's request ----
+  ctl.begin_solve();
+  const bool live_best = o.live_best && world > 1;
+  e.set_progress_hook([&](size_t pool, int& best) {
     ctl.publish_size(static_cast<int64_t>(pool));
+    if (live_best) best = std::min(best, ctl.exchange_best(best));
     return board && ctl.round_requested();
   });
   struct Unhook {
@@ -244,7 +259,15 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     ~Unhook() { e.set_progress_hook(nullptr); }
   } unhook{e};
 
-  std::vector<int64_t> st(static_cast<size_t>(world) * 3), sizes(world);
+  constexpr int kRec = 4;  // status record: pool size, incumbent, split pending, time up
+  std::vector<int64_t> st(static_cast<size_t>(world) * kRec), sizes(world);
+  const auto t_begin = clock::now();
+  const int lw = o.local_world > 0 ? o.local_world : std::max(1, world);
+  // ranks that may donate to this one (the pair filter of plan_transfers)
+  auto eligible = [&](int q) {
+    const bool same = q / lw == rank / lw;
+    return q != rank && ((o.intra && same) || (o.inter && !same));
+  };
   for (;;) {
     const auto t0 = clock::now();
     beat(0);
@@ -268,7 +291,7 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     auto want_work = [&]() {
       if (!board || asked || !needy || pend) return false;
       for (int q = 0; q < world; ++q)
-        if (q != rank && ctl.peer_size(q) >= static_cast<int64_t>(o.donor_min)) return true;
+        if (eligible(q) && ctl.peer_size(q) >= static_cast<int64_t>(o.donor_min)) return true;
       return false;
     };
     if (want_work()) {
@@ -276,10 +299,11 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
       asked = true;
       ++early;
     }
-    const int64_t mine[3] = {size, mybest, pend ? 1 : 0};
+    const bool timeup = o.time_limit > 0 && secs(t_begin, clock::now()) >= o.time_limit;
+    const int64_t mine[kRec] = {size, mybest, pend ? 1 : 0, timeup ? 1 : 0};
     {
       TTS_RANGE("tts.dist.round");
-      ctl.allgather(mine, 3, st.data(), [&] {
+      ctl.allgather(mine, kRec, st.data(), [&] {
         if (want_work()) {
           ctl.request_current_round();
           asked = true;
@@ -292,11 +316,12 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     bool replicated = false;
     int gbest = mybest;
     int64_t total = 0;
-    bool starving = false;
+    bool starving = false, out_of_time = false;
     for (int r = 0; r < world; ++r) {
-      sizes[r] = st[r * 3];
-      gbest = std::min<int>(gbest, static_cast<int>(st[r * 3 + 1]));
-      replicated |= st[r * 3 + 2] != 0;
+      sizes[r] = st[r * kRec];
+      gbest = std::min<int>(gbest, static_cast<int>(st[r * kRec + 1]));
+      replicated |= st[r * kRec + 2] != 0;
+      out_of_time |= st[r * kRec + 3] != 0;
       total += sizes[r];
       starving |= sizes[r] < static_cast<int64_t>(o.needy_below);
     }
@@ -305,6 +330,11 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     if (total == 0) {  // every pool is empty and nothing is in flight: exact termination
       t_term += secs(t1, clock::now());
       t_comm += secs(t1, clock::now());
+      break;
+    }
+    if (out_of_time) {  // time box over on some rank: every rank stops at this round
+      t_comm += secs(t1, clock::now());
+      out.complete = false;
       break;
     }
     if (share && starving && !replicated) {

@@ -53,21 +53,49 @@ struct DistSolveResult {
   DistOutcome outcome;
 };
 
-// Every rank: the same warm-up to `warm_target` nodes, the split armed at `split_min`
-// pool nodes (IEngine::set_split), the rounds, then global counts (Step-1 counts once).
-// A world of one is the engine's fused solve from the warm-up (bench.py at N = 1).
+// Rank-strided share of the warm-up nodes: i = rank, rank + world, ...; the last rank
+// also takes the tail (ref Pool_atom.c:14-36 roundRobin_distribution).
+inline void keep_round_robin(WarmupResult& w, size_t node_bytes, int rank, int world) {
+  const size_t c = w.n / static_cast<size_t>(world);
+  std::vector<uint8_t> mine;
+  mine.reserve((c + static_cast<size_t>(world)) * node_bytes);
+  auto take = [&](size_t i) { mine.insert(mine.end(), w.nodes.begin() + i * node_bytes, w.nodes.begin() + (i + 1) * node_bytes); };
+  for (size_t k = 0; k < c; ++k) take(static_cast<size_t>(rank) + k * static_cast<size_t>(world));
+  if (rank == world - 1)
+    for (size_t i = c * static_cast<size_t>(world); i < w.n; ++i) take(i);
+  w.n = mine.size() / node_bytes;
+  w.nodes.swap(mine);
+}
+
+// Every rank: the same warm-up to `warm_target` nodes, then either the split armed at
+// `split_min` pool nodes (IEngine::set_split, split = true) or the round-robin share
+// of the warm-up nodes (split = false, ref roundRobin_distribution), the rounds, then
+// global counts (Step-1 counts once). A world of one is the engine's fused solve from
+// the warm-up (bench.py at N = 1); with o.time_limit it is a time box instead
+// (complete = false when the pool was not exhausted).
 inline DistSolveResult dist_solve_split(IEngine& e, RoundControl& ctl, const DistOptions& o, const WarmupFn& warm,
                                         int best, size_t warm_target, size_t split_min, const TransferFn& xfer,
-                                        const RoundHook& hook) {
+                                        const RoundHook& hook, bool split = true) {
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
   WarmupResult w = warm(best, warm_target);
   if (ctl.world() == 1) {
     // one rank: the engine's own fused solve (no rounds, no control plane)
     const auto t1 = clock::now();
-    const EngineStats st = e.solve_from(w.nodes.data(), w.n, w.best);
+    EngineStats st;
+    bool complete = true;
+    if (o.time_limit > 0) {
+      e.begin(w.nodes.data(), w.n, w.best);
+      e.run(-1, o.time_limit, 0);
+      st = e.stats();
+      complete = e.size() == 0;
+    } else {
+      st = e.solve_from(w.nodes.data(), w.n, w.best);
+    }
     const auto t2 = clock::now();
     DistSolveResult r;
+    r.complete = complete;
+    r.outcome.complete = complete;
     r.best = std::min(st.best, w.best);
     r.tree = w.tree + st.tree;
     r.sol = w.sol + st.sol;
@@ -88,7 +116,10 @@ inline DistSolveResult dist_solve_split(IEngine& e, RoundControl& ctl, const Dis
     for (auto* v : {&o1.t_comm, &o1.t_idle, &o1.t_termination, &o1.t_load_bal}) one(*v, 0.0);
     return r;
   }
-  e.set_split(ctl.rank(), ctl.world(), split_min);
+  if (split)
+    e.set_split(ctl.rank(), ctl.world(), split_min);
+  else
+    keep_round_robin(w, e.node_bytes(), ctl.rank(), ctl.world());
   e.begin(w.nodes.data(), w.n, w.best);
   const auto t1 = clock::now();
   DistSolveResult r;

@@ -11,10 +11,13 @@
 namespace tts {
 
 // Called by run() between two graph replays (nothing in flight) with the current
-// pool size; returning true ends run() early. The distributed runtime uses it to
-// publish its pool size on the node-wide board and to answer a peer's early
-// round request (core/dist_rounds.hpp).
-using ProgressHook = std::function<bool(size_t pool)>;
+// pool size and the engine's incumbent; returning true ends run() early. The hook
+// may lower `best` (a peer found a better solution): the engine adopts it before
+// its next replay. The distributed runtime uses it to publish its pool size and
+// incumbent on the node-wide board, to pull the node-wide incumbent (ref
+// checkBest around every batch, pfsp_multigpu_cuda.c:30-50,307-312) and to answer
+// a peer's early round request (core/dist_rounds.hpp).
+using ProgressHook = std::function<bool(size_t pool, int& best)>;
 
 struct EngineConfig {
   int device = 0;

@@ -163,6 +163,7 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
   std::vector<std::atomic<size_t>> live(W);
   for (auto& x : live) x.store(0);
   std::atomic<unsigned long long> request{0};
+  std::atomic<int> live_best{best};  // node-wide incumbent, exchanged after every replay
   double slice = cfg.slice_min;
   RoundBarrier bar(W);
   std::mutex stage_mu;
@@ -241,9 +242,15 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
     const std::vector<uint8_t>& init = initial[w];
     guarded([&] { e->begin(init.data(), init.size() / nb, best); });
     // early rounds (as in dist_rounds.hpp): publish the live pool size after every
-    // replay; leave the slice when a dry worker asked for the next round
-    e->set_progress_hook([&, w](size_t pool) {
+    // replay and exchange the incumbent with every worker (ref checkBest before and
+    // after every batch, pfsp_multigpu_cuda.c:30-50,307-312); leave the slice when a
+    // dry worker asked for the next round
+    e->set_progress_hook([&, w](size_t pool, int& b) {
       live[w].store(pool, std::memory_order_relaxed);
+      int cur = live_best.load(std::memory_order_acquire);
+      while (b < cur && !live_best.compare_exchange_weak(cur, b, std::memory_order_acq_rel)) {
+      }
+      if (cur < b) b = cur;
       return cfg.work_sharing && request.load(std::memory_order_acquire) > rep[w].rounds;
     });
     for (;;) {
@@ -356,7 +363,12 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
         beat(w, Phase::Transfer);
         size_t in = 0;
         if (dcount[w]) {
-          guarded([&] { e->import_device(dbuf[w], dcount[w]); });
+          // the copy out of dbuf[w] completes before the round ends: a later round's
+          // donor may overwrite dbuf[w] as soon as it passes the next barrier
+          guarded([&] {
+            e->import_device(dbuf[w], dcount[w]);
+            e->fence();
+          });
           in += dcount[w];
           dcount[w] = 0;
         }

@@ -159,6 +159,24 @@ class ShmControl {
   }
   int64_t best() const { return hdr_->best.load(std::memory_order_acquire); }
 
+  // Live incumbent of the current cooperative solve, exchanged after every graph
+  // replay (not only at round boundaries). The word is (solve epoch << 32) | best,
+  // so a solve never inherits the previous solve's incumbent: every rank calls
+  // begin_solve() once per solve, in the same order, like the all-gathers.
+  uint32_t begin_solve() { return ++epoch_; }
+  int exchange_best(int b) {
+    if (epoch_ == 0) return b;  // no solve begun: nothing to exchange with
+    const uint64_t mine = (static_cast<uint64_t>(epoch_) << 32) | static_cast<uint32_t>(b);
+    uint64_t cur = hdr_->solve_best.load(std::memory_order_acquire);
+    for (;;) {
+      const uint32_t ce = static_cast<uint32_t>(cur >> 32);
+      const int cb = static_cast<int>(static_cast<uint32_t>(cur));
+      if (ce > epoch_) return b;               // a peer has already moved on to the next solve
+      if (ce == epoch_ && cb <= b) return cb;  // a peer's incumbent is at least as good
+      if (hdr_->solve_best.compare_exchange_weak(cur, mine, std::memory_order_acq_rel)) return b;
+    }
+  }
+
   // ---- board ----
   void publish_size(int64_t n) { board_[rank_].size.store(n, std::memory_order_relaxed); }
   int64_t peer_size(int r) const { return board_[r].size.load(std::memory_order_relaxed); }
@@ -184,6 +202,7 @@ class ShmControl {
     int pad;
     std::atomic<int64_t> best;
     std::atomic<uint64_t> request;  // highest all-gather round requested early
+    std::atomic<uint64_t> solve_best;  // (solve epoch << 32) | live incumbent (exchange_best)
   };
   struct alignas(128) Board {
     std::atomic<int64_t> size;  // live pool size of the rank
@@ -205,6 +224,7 @@ class ShmControl {
   Board* board_ = nullptr;
   Slot* slots_ = nullptr;
   uint64_t round_ = 0;
+  uint32_t epoch_ = 0;  // cooperative solves begun (begin_solve)
   uint64_t tag_ = layout_tag();
 };
 

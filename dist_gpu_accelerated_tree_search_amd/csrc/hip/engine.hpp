@@ -329,7 +329,15 @@ class DeviceEngine final : public IEngine {
       if (all < stop_below) break;
       if (max_launches >= 0 && launches >= max_launches) break;
       if (max_seconds > 0 && elapsed() >= max_seconds) break;
-      if (hook_ && hook_(all)) break;
+      if (hook_) {
+        int b = h_ctl_->best.v;
+        const bool stop = hook_(all, b);
+        if (b < h_ctl_->best.v) {  // a peer's better incumbent: prune with it from the next replay on
+          h_ctl_->best.v = b;
+          upload_ctl();
+        }
+        if (stop) break;
+      }
       // refill ahead of need from the pinned spill, one pinned block at a time, while
       // the device still holds work for the next replays to overlap the copy with
       const size_t low = std::max(4 * cfg_.max_parents, spill_.block_nodes() / 2);

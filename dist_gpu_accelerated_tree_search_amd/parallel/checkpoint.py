@@ -63,6 +63,7 @@ def load_all(directory: str, model) -> tuple[np.ndarray, int, int, int, int]:
         raise ValueError(f"mixed checkpoints in {directory}: worlds {sorted(worlds)}")
     world = worlds.pop()
     nodes, tree, sol, best, rounds = [], 0, 0, 2**31 - 1, 0
+    seen_rounds = set()
     for r in range(world):
         f = _path(directory, r, world)
         with np.load(f, allow_pickle=False) as z:
@@ -77,5 +78,11 @@ def load_all(directory: str, model) -> tuple[np.ndarray, int, int, int, int]:
             sol += int(meta[1])
             best = min(best, int(meta[2]))
             rounds = max(rounds, int(meta[3]))
+            seen_rounds.add(int(meta[3]))
+    if len(seen_rounds) > 1:
+        # a crash between two ranks' writes of one periodic checkpoint leaves files of
+        # different rounds: resuming from them would lose or duplicate subtrees
+        raise ValueError(f"inconsistent checkpoint in {directory}: ranks saved different rounds "
+                         f"{sorted(seen_rounds)}")
     allnodes = np.concatenate(nodes) if nodes else np.zeros((0, model.node_bytes), np.uint8)
     return allnodes, tree, sol, best, rounds

@@ -98,8 +98,69 @@ class Comm:
         self._staging = {}
         if shm_control_wanted(self.topo):
             self.ctl = self._open_shm_control()
+        self.preflight = None
         if self.distributed and use_gpu and self.backend == "nccl":
             self._connect_peers()
+            if os.environ.get("TTS_P2P_PREFLIGHT", "1") != "0":
+                self.preflight = self.preflight_p2p()
+
+    def preflight_p2p(self, nbytes: int = 4 << 20) -> dict:
+        """Check the node-transfer path end to end before any solve relies on it.
+
+        Every rank sends a rank-stamped pattern of `nbytes` to every peer and receives
+        one from each, through the same grouped isend/irecv (`_p2p`) that
+        execute_transfers uses, enqueued on a side stream wrapped as an external stream
+        exactly like the engine's transfer stream. Each received buffer is compared
+        word for word with the pattern its sender must have written; a mismatch or a
+        failed call raises with the peers involved (no silent fallback, no restart).
+        Returns {"ok", "peers", "bytes_per_peer", "seconds", "GBps"} (GBps: bytes this
+        rank received per second over all its links). With gloo the buffers are host
+        tensors (CPU tests drive the same code)."""
+        if not self.distributed:
+            return {"ok": True, "peers": 0, "bytes_per_peer": 0, "seconds": 0.0, "GBps": 0.0}
+        torch = self.torch
+        me, n = self.rank, self.world
+        peers = [p for p in range(n) if p != me]
+        words = max(1, int(nbytes) // 4)
+        nccl = self.backend == "nccl"
+        dev = self.device if nccl else torch.device("cpu")
+
+        def pattern(src: int, dst: int):
+            i = torch.arange(words, dtype=torch.int64, device=dev)
+            v = (i * 2654435761 + src * 0x9E3779B1 + dst * 0x85EBCA77 + 12345) & 0x7FFFFFFF
+            return v.to(torch.int32)
+
+        ctx = None
+        if nccl:
+            side = torch.cuda.Stream(device=dev)
+            ctx = torch.cuda.ExternalStream(side.cuda_stream, device=dev)
+        import contextlib
+        import time as _time
+
+        with (torch.cuda.stream(ctx) if ctx is not None else contextlib.nullcontext()):
+            src = torch.cat([pattern(me, p) for p in peers]).view(torch.uint8)
+            dst = torch.zeros(len(peers) * words, dtype=torch.int32, device=dev).view(torch.uint8)
+            plan_out = [(p, words) for p in peers]
+            plan_in = [(p, words) for p in peers]
+            if nccl:
+                ctx.synchronize()
+            t0 = _time.perf_counter()
+            try:
+                self._p2p(plan_out, plan_in, src, dst, 4)
+                if nccl:
+                    ctx.synchronize()
+            except Exception as e:  # noqa: BLE001 - re-raised with context
+                raise RuntimeError(f"rank {me}: {self.backend} point-to-point preflight failed "
+                                   f"({len(peers)} peers, {words * 4} B each): {e}") from e
+            dt = _time.perf_counter() - t0
+            got = dst.view(torch.int32).reshape(len(peers), words)
+            bad = [p for k, p in enumerate(peers) if not torch.equal(got[k], pattern(p, me))]
+        if bad:
+            raise RuntimeError(f"rank {me}: {self.backend} point-to-point preflight: data received from "
+                               f"rank(s) {bad} does not match what they sent; node transfers over this "
+                               "backend would corrupt the pools")
+        return {"ok": True, "peers": len(peers), "bytes_per_peer": words * 4, "seconds": dt,
+                "GBps": len(peers) * words * 4 / max(dt, 1e-9) / 1e9}
 
     def _connect_peers(self) -> None:
         """RCCL sets up a point-to-point channel on first use; do it for every pair now

@@ -79,6 +79,12 @@ class DistConfig:
     checkpoint_every: int = 0
     max_rounds: int = 0
     resume: bool = False
+    # throughput time box: every rank stops at the first round after time_limit_s
+    # seconds on any rank (result.extra["complete"] is then False); 0: solve to the end
+    time_limit_s: float = 0.0
+    # exchange the incumbent through the node-wide board after every graph replay
+    # (ref checkBest around every batch); False: only at round boundaries
+    live_best: bool = True
     # failure detection / fault injection (parallel/faults.py; env TTS_FAULT_*)
     watchdog_s: float = 0.0
     watchdog_abort: bool = False
@@ -132,7 +138,7 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
     else:
         mine = np.ascontiguousarray(nodes[round_robin_share(len(nodes), rank, world)])
     t_init = time.perf_counter() - t_start
-    if world == 1 and not cfg.max_rounds and not cfg.checkpoint_dir:  # one fused native solve, no rounds
+    if world == 1 and not cfg.max_rounds and not cfg.checkpoint_dir and not cfg.time_limit_s:  # one fused solve
         st = engine.solve(mine, int(best))
         elapsed = time.perf_counter() - t_start
         w = WorkerStats(tree=int(st["tree"]), sol=int(st["sol"]), gen_child=int(st["tree"]),
@@ -193,6 +199,7 @@ def _native_options(cfg: DistConfig, engine, comm: Comm, window: int | None):
     opts = dict(needy_below=needy, donor_min=donor, steal_cap=cfg.steal_cap, slice_min=cfg.slice_min_s,
                 slice_max=cfg.slice_max_s, intra=bool(cfg.ws and share), inter=bool(cfg.L and share),
                 local_world=comm.topo.local_world, early_rounds=cfg.early_rounds, max_rounds=cfg.max_rounds,
+                time_limit=float(cfg.time_limit_s), live_best=bool(cfg.live_best),
                 checkpoint_every=cfg.checkpoint_every if cfg.checkpoint_dir else 0,
                 watchdog_s=float(cfg.watchdog_s or float(env.get("TTS_WATCHDOG_S", "0") or 0)),
                 watchdog_abort=bool(cfg.watchdog_abort or env.get("TTS_WATCHDOG_ABORT", "0") not in ("", "0")),
@@ -307,10 +314,13 @@ class DistSolver:
         shm = comm.control_address(mod)
         world = comm.world
         split = cfg.split and world > 1
+        # Step 1: with the in-search split every rank starts from the 1-rank warm-up
+        # (init_per_rank nodes); without it, a host BFS to world * init_per_rank nodes
+        # and the round-robin share (ref roundRobin_distribution)
+        warm = cfg.init_per_rank if split else world * cfg.init_per_rank
         self._s = mod.DistSession(engine, model, shm, None if shm else comm.allgather_i64, comm.rank, world, opts,
                                   lambda plan: comm.execute_transfers(plan, engine, model.node_bytes), None,
-                                  int(cfg.m if split or world == 1 else world * cfg.init_per_rank),
-                                  int(cfg.split_per_rank * world), float(comm.timeout_s))
+                                  int(warm), int(cfg.split_per_rank * world), float(comm.timeout_s), bool(split))
 
     def solve_raw(self, ub: int = 1) -> tuple:
         """(best, tree, sol, rounds, complete, t_init, t_search, elapsed), global values."""

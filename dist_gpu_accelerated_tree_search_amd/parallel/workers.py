@@ -52,3 +52,27 @@ def solve_rank(spec: dict) -> dict:
     finally:
         comm.barrier()
         comm.close()
+
+
+def preflight_rank(spec: dict) -> dict:
+    """Point-to-point preflight (Comm.preflight_p2p) on the current process group;
+    spec["corrupt_rank"] makes that rank's received data wrong (test of the check)."""
+    use_gpu = spec.get("backend", "cpu") == "gpu" and spec.get("comm", "nccl") == "nccl"
+    comm = Comm(use_gpu=use_gpu)
+    try:
+        bad = spec.get("corrupt_rank")
+        if bad is not None and comm.rank == int(bad):
+            real = comm._p2p
+
+            def corrupt(outgoing, incoming, src, dst, nb):
+                real(outgoing, incoming, src, dst, nb)
+                dst[0] ^= 1
+
+            comm._p2p = corrupt
+        try:
+            return {"rank": comm.rank, "ok": True, "info": comm.preflight_p2p(int(spec.get("nbytes", 1 << 16)))}
+        except RuntimeError as e:
+            return {"rank": comm.rank, "ok": False, "error": str(e)}
+    finally:
+        comm.barrier()
+        comm.close()

@@ -1,0 +1,119 @@
+"""Round-3 runtime features on CPU ranks (gloo): the point-to-point preflight, time
+boxes, the live incumbent exchange, the round-robin Step 1 of the native session,
+checkpoint consistency, and bench.py's extras path (the other BASELINE configs run
+in the same job as the headline)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from dist_gpu_accelerated_tree_search_amd.parallel.launch import free_port, spawn_local
+from dist_gpu_accelerated_tree_search_amd.parallel.workers import preflight_rank, solve_rank
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = (2573652, 2648, 1377)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_p2p_preflight_passes(world):
+    res = spawn_local(world, preflight_rank, ({"nbytes": 1 << 15},), timeout=120)
+    for r in res:
+        assert r["ok"], r
+        assert r["info"]["peers"] == world - 1 and r["info"]["bytes_per_peer"] == 1 << 15
+
+
+def test_p2p_preflight_detects_corruption():
+    res = spawn_local(3, preflight_rank, ({"nbytes": 1 << 12, "corrupt_rank": 1},), timeout=120)
+    assert res[0]["ok"] and res[2]["ok"]
+    assert not res[1]["ok"] and "does not match" in res[1]["error"] and "[0]" in res[1]["error"]
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_time_box_stops_every_rank(world):
+    # ta056 LB2 cannot finish: the session stops at the first round after the box on
+    # every rank, reports complete=False and the nodes explored so far
+    spec = {"problem": "pfsp", "inst": 56, "lb": 2, "backend": "cpu", "session": True,
+            "dist": {"time_limit_s": 0.3}}
+    res = spawn_local(world, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert r["extra"]["complete"] is False
+        assert r["tree"] > 0 and r["best"] == 3679
+        assert r["t_search"] < 30
+    assert len({r["tree"] for r in res}) == 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_session_round_robin_step1(world):
+    # split=False: host BFS to world * init_per_rank nodes, rank-strided share
+    # (ref roundRobin_distribution), then the rounds; golden tree
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu", "session": True, "repeat": 2,
+            "dist": {"split": False, "init_per_rank": 16}}
+    res = spawn_local(world, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == GOLD
+    assert all(w["tree"] > 0 for w in res[0]["workers"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_live_incumbent_with_unknown_optimum(world):
+    # -u 0: the optimum must be found whatever the exchange; with the live exchange a
+    # rank's better solution prunes the other ranks' pools between rounds too
+    trees = {}
+    for live in (False, True):
+        spec = {"problem": "pfsp", "inst": 2, "lb": 0, "backend": "cpu", "ub": 0, "session": True,
+                "dist": {"live_best": live}}
+        res = spawn_local(world, solve_rank, (spec,), timeout=300)
+        assert all(r["best"] == 1359 for r in res)
+        trees[live] = res[0]["tree"]
+    assert trees[True] > 0 and trees[False] > 0
+
+
+def test_checkpoint_rejects_mixed_rounds(tmp_path):
+    from dist_gpu_accelerated_tree_search_amd.models.pfsp import PfspModel
+    from dist_gpu_accelerated_tree_search_amd.parallel import checkpoint as ckpt
+
+    model = PfspModel(14, 0)
+    eng = model.make_engine("cpu")
+    eng.begin(model.root(), 1377)
+    eng.run(3)
+    ckpt.save(str(tmp_path), 0, 2, model, eng, 10, 0, 1377, 5)
+    ckpt.save(str(tmp_path), 1, 2, model, eng, 10, 0, 1377, 4)  # crashed before rewriting round 5
+    with pytest.raises(ValueError, match="different rounds"):
+        ckpt.load_all(str(tmp_path), model)
+    ckpt.save(str(tmp_path), 1, 2, model, eng, 10, 0, 1377, 5)
+    nodes, tree, sol, best, rounds = ckpt.load_all(str(tmp_path), model)
+    assert rounds == 5 and tree == 20 and len(nodes) == 2 * eng.size()
+    assert isinstance(nodes, np.ndarray)
+
+
+def test_bench_extras_cpu_gloo():
+    # the driver's launch line with 2 ranks (CPU engines, gloo): one JSON line with the
+    # headline and both extras; small stand-ins keep it short (ta014 for the complete
+    # LB1_d solve, a 0.5-s ta056 LB2 box)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
+           "--steps", "1", "--warmup", "0", "--backend", "cpu", "--comm", "gloo", "--extra-inst-lb1d", "14",
+           "--box-s", "0.5"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and (rec["config"]["tree"], rec["config"]["sol"], rec["config"]["makespan"]) == GOLD
+    ex = rec["extras"]
+    assert (ex["ta021"]["tree"], ex["ta021"]["sol"], ex["ta021"]["makespan"]) == GOLD
+    assert ex["ta021"]["complete"] is True
+    assert ex["ta056"]["complete"] is False and ex["ta056"]["nodes_per_s"] > 0
+    assert ex["ta056"]["time_box_s"] == 0.5
+
+
+def test_bench_extras_failure_still_prints_headline():
+    # an extra that fails is reported in the line; the headline is printed regardless
+    cmd = [sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--backend", "cpu", "--extras", "nosuch"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][0])
+    assert rec["value"] > 0 and rec["extras"]["nosuch"] == {"error": "unknown extra"}

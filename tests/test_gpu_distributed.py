@@ -53,3 +53,32 @@ def test_gpu_skewed_start_is_balanced_through_device_staging():
     assert sum(r["comm"]["device_transfers"] for r in res) > 0
     assert sum(r["comm"]["host_transfers"] for r in res) == 0
     assert sum(res[0]["extra"]["sent_nodes"]) == sum(res[0]["extra"]["received_nodes"]) > 0
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_gpu_time_box(world):
+    # bench.py's ta056 extra: a time-boxed LB2 solve stops on every rank together
+    spec = {"problem": "pfsp", "inst": 56, "lb": 2, "backend": "gpu", "comm": "gloo", "device": 0, "session": True,
+            "engine": {"ring_bytes": 1 << 30}, "dist": {"time_limit_s": 0.5}}
+    res = spawn_local(world, solve_rank, (spec,), timeout=600)
+    for r in res:
+        assert r["extra"]["complete"] is False and r["tree"] > 0 and r["best"] == 3679
+        assert r["t_search"] < 5.0
+
+
+def test_gpu_session_round_robin_step1():
+    spec = {"problem": "pfsp", "inst": 14, "lb": 1, "backend": "gpu", "comm": "gloo", "device": 0, "session": True,
+            "repeat": 2, "engine": {"ring_bytes": 1 << 28, "max_parents": 1 << 16},
+            "dist": {"split": False, "init_per_rank": 64}}
+    res = spawn_local(2, solve_rank, (spec,), timeout=600)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == (2573652, 2648, 1377)
+
+
+@pytest.mark.parametrize("live", [False, True])
+def test_gpu_unknown_optimum_multi_rank(live):
+    # -u 0 on 2 ranks: the optimum is found with and without the live incumbent exchange
+    spec = {"problem": "pfsp", "inst": 14, "lb": 1, "backend": "gpu", "comm": "gloo", "device": 0, "session": True,
+            "ub": 0, "engine": {"ring_bytes": 1 << 30, "max_parents": 1 << 16}, "dist": {"live_best": live}}
+    res = spawn_local(2, solve_rank, (spec,), timeout=600)
+    assert all(r["best"] == 1377 for r in res)
