@@ -55,18 +55,17 @@ int main(int argc, char* argv[]) {
     owned.push_back(make_pfsp_engine(in, a.lb, cfg));
   }
   const int host_lb = a.lb == 1 ? 0 : a.lb;  // ref: CPU workers use LB1_d for LB1
-  return with_pfsp_bucket(in.jobs, [&](auto nj) {
-    constexpr int NJ = decltype(nj)::value;
-    using Node = PfspNode<NJ>;
-    if (cpu_threads > 0)
-      owned.push_back(std::make_unique<CpuEngine<PfspProblem<NJ>>>(PfspProblem<NJ>(in, host_lb), a.T, cpu_threads));
+  // the engines' node layout (front nodes for LB1 / LB1_d on 20-job instances)
+  return with_pfsp_problem(in, host_lb, [&](auto prob) {
+    using Problem = decltype(prob);
+    using Node = typename Problem::Node;
+    if (cpu_threads > 0) owned.push_back(std::make_unique<CpuEngine<Problem>>(prob, a.T, cpu_threads));
     std::vector<IEngine*> engines;
     for (auto& e : owned) engines.push_back(e.get());
     const int W = static_cast<int>(engines.size());
 
     // Step 1: host breadth-first warm-up to W*m nodes
     const double t0 = now_s();
-    PfspProblem<NJ> prob(in, host_lb);
     Pool<Node> pool;
     pool.push_back_free(prob.root());
     u64 tree = 0, sol = 0;

@@ -43,10 +43,6 @@ inline py::dict engine_stats_dict(const EngineStats& s) {
   d["exports"] = s.exports;
   d["imports"] = s.imports;
   d["pinned_bytes"] = s.pinned_bytes;
-  d["p_steps"] = s.p_steps;
-  d["p_donations"] = s.p_donations;
-  d["p_waits"] = s.p_waits;
-  d["p_wait_us"] = s.p_wait_us;
   return d;
 }
 

@@ -8,6 +8,7 @@
 #include "../core/cpu_engine.hpp"
 #include "../core/drivers_cpu.hpp"
 #include "../core/estimate.hpp"
+#include "../core/pfsp_front.hpp"
 #include "../core/shm_control.hpp"
 #include "engine_binding.hpp"
 
@@ -127,6 +128,69 @@ PYBIND11_MODULE(_tts_cpu, m) {
     return with_pfsp_bucket(jobs, [](auto nj) { return sizeof(PfspNode<decltype(nj)::value>); });
   });
   m.def("pfsp_bucket", &pfsp_bucket);
+  // node layout of the engines for (instance, lb): front nodes where they apply
+  // (core/pfsp_front.hpp), else the permutation node of the job-count bucket
+  m.def("pfsp_engine_node_bytes", [](const PfspInstance& in, int lb) {
+    return with_pfsp_problem(in, lb, [](auto prob) { return sizeof(typename decltype(prob)::Node); });
+  });
+  m.def("pfsp_front_layout", [](const PfspInstance& in, int lb) { return pfsp_front_ok(in, lb); });
+  m.def(
+      "pfsp_root",
+      [](const PfspInstance& in, int lb) {
+        return with_pfsp_problem(in, lb, [](auto prob) {
+          const auto r = prob.root();
+          return nodes_to_array(&r, 1);
+        });
+      },
+      py::arg("inst"), py::arg("lb"), "Root node in the engines' layout, shape (1, node_bytes).");
+  m.def(
+      "pfsp_to_engine_layout",
+      [](const PfspInstance& in, int lb, U8 nodes) {
+        // permutation-layout nodes (utils/nodes.pfsp_pack) -> the engines' layout
+        return with_pfsp_bucket(in.jobs, [&](auto nj) -> U8 {
+          constexpr int NJ = decltype(nj)::value;
+          size_t n = 0;
+          const PfspNode<NJ>* p = array_nodes<PfspNode<NJ>>(nodes, n);
+          if (!pfsp_front_ok(in, lb)) return nodes_to_array(p, n);
+          return with_pfsp_problem(in, lb, [&](auto prob) -> U8 {
+            using P = decltype(prob);
+            if constexpr (is_front_problem<P>::value && NJ == 20) {
+              std::vector<typename P::Node> out(n);
+              for (size_t i = 0; i < n; ++i) out[i] = pfsp_front_from_perm(prob, p[i]);
+              return nodes_to_array(out.data(), n);
+            } else {
+              return nodes_to_array(p, n);
+            }
+          });
+        });
+      },
+      py::arg("inst"), py::arg("lb"), py::arg("nodes"));
+  m.def(
+      "pfsp_children_bounds",
+      [](const PfspInstance& in, int lb, U8 nodes) {
+        // bounds of every child of engine-layout nodes, by ascending job id per node
+        // (front layout) or child position (permutation layout): the host twin of the
+        // front kernel, for tests
+        std::vector<int> out;
+        with_pfsp_problem(in, lb, [&](auto prob) {
+          using P = decltype(prob);
+          using Node = typename P::Node;
+          size_t n = 0;
+          const Node* p = array_nodes<Node>(nodes, n);
+          for (size_t i = 0; i < n; ++i) {
+            if constexpr (is_front_problem<P>::value) {
+              int by_job[32];
+              prob.children_bounds(p[i], by_job);
+              for (uint32_t x = p[i].rest; x; x &= x - 1) out.push_back(by_job[__builtin_ctz(x)]);
+            } else {
+              throw std::invalid_argument("pfsp_children_bounds: front layout only");
+            }
+          }
+          return 0;
+        });
+        return out;
+      },
+      py::arg("inst"), py::arg("lb"), py::arg("nodes"));
   m.def("queens_node_bytes", []() { return sizeof(QueensNode); });
 
   // ---- end-to-end CPU drivers ----
@@ -156,10 +220,8 @@ PYBIND11_MODULE(_tts_cpu, m) {
   m.def(
       "pfsp_bfs",
       [](const PfspInstance& in, int lb, int best, size_t target) {
-        return with_pfsp_bucket(in.jobs, [&](auto nj) {
-          constexpr int NJ = decltype(nj)::value;
-          PfspProblem<NJ> prob(in, lb);
-          Pool<PfspNode<NJ>> pool;
+        return with_pfsp_problem(in, lb, [&](auto prob) {
+          Pool<typename decltype(prob)::Node> pool;
           pool.push_back_free(prob.root());
           u64 tree = 0, sol = 0;
           bfs_warmup(prob, pool, target, best, tree, sol);
@@ -232,10 +294,7 @@ PYBIND11_MODULE(_tts_cpu, m) {
           const PfspInstance& in = problem.attr("native").cast<const PfspInstance&>();
           const int lb = problem.attr("host_lb").cast<int>();
           py::gil_scoped_release nogil;
-          e = with_pfsp_bucket(in.jobs, [&](auto nj) {
-            constexpr int NJ = decltype(nj)::value;
-            return knuth_estimate(PfspProblem<NJ>(in, lb), best, probes, seed, threads);
-          });
+          e = with_pfsp_problem(in, lb, [&](auto prob) { return knuth_estimate(prob, best, probes, seed, threads); });
         } else {
           QueensProblem q(problem.attr("N").cast<int>(), problem.attr("G").cast<int>());
           py::gil_scoped_release nogil;
@@ -248,10 +307,8 @@ PYBIND11_MODULE(_tts_cpu, m) {
   m.def(
       "pfsp_drain",
       [](const PfspInstance& in, int lb, int best, U8 nodes) {
-        return with_pfsp_bucket(in.jobs, [&](auto nj) {
-          constexpr int NJ = decltype(nj)::value;
-          using Node = PfspNode<NJ>;
-          PfspProblem<NJ> prob(in, lb);
+        return with_pfsp_problem(in, lb, [&](auto prob) {
+          using Node = typename decltype(prob)::Node;
           size_t n = 0;
           const Node* p = array_nodes<Node>(nodes, n);
           Pool<Node> pool;
@@ -299,9 +356,8 @@ PYBIND11_MODULE(_tts_cpu, m) {
   m.def(
       "make_pfsp_cpu_engine",
       [](const PfspInstance& in, int lb, size_t batch, int threads) -> std::unique_ptr<IEngine> {
-        return with_pfsp_bucket(in.jobs, [&](auto nj) -> std::unique_ptr<IEngine> {
-          constexpr int NJ = decltype(nj)::value;
-          return std::make_unique<CpuEngine<PfspProblem<NJ>>>(PfspProblem<NJ>(in, lb), batch, threads);
+        return with_pfsp_problem(in, lb, [&](auto prob) -> std::unique_ptr<IEngine> {
+          return std::make_unique<CpuEngine<decltype(prob)>>(prob, batch, threads);
         });
       },
       py::arg("inst"), py::arg("lb"), py::arg("batch") = 4096, py::arg("threads") = 1, py::keep_alive<0, 1>());
@@ -317,10 +373,7 @@ PYBIND11_MODULE(_tts_cpu, m) {
     if (py::hasattr(model, "native")) {
       auto inst = std::make_shared<PfspInstance>(model.attr("native").cast<const PfspInstance&>());
       const int lb = model.attr("host_lb").cast<int>();
-      return with_pfsp_bucket(inst->jobs, [&](auto nj) -> WarmupFn {
-        constexpr int NJ = decltype(nj)::value;
-        return make_warmup(inst, PfspProblem<NJ>(*inst, lb));
-      });
+      return with_pfsp_problem(*inst, lb, [&](auto prob) -> WarmupFn { return make_warmup(inst, prob); });
     }
     return make_warmup(nullptr, QueensProblem(model.attr("N").cast<int>(), model.attr("G").cast<int>()));
   });

@@ -9,6 +9,7 @@
 #include <string>
 
 #include "../core/cpu_engine.hpp"
+#include "../core/pfsp_front.hpp"
 #include "../core/problems.hpp"
 #include "../hip/host_support.hpp"
 #include "../hip/pfsp_engine.hpp"
@@ -48,10 +49,7 @@ PYBIND11_MODULE(_tts_hip, m) {
                                                                model.attr("machines").cast<int>(),
                                                                model.attr("native").attr("p").cast<std::vector<int>>()));
       const int lb = model.attr("host_lb").cast<int>();
-      return with_pfsp_bucket(inst->jobs, [&](auto nj) -> WarmupFn {
-        constexpr int NJ = decltype(nj)::value;
-        return make_warmup(inst, PfspProblem<NJ>(*inst, lb));
-      });
+      return with_pfsp_problem(*inst, lb, [&](auto prob) -> WarmupFn { return make_warmup(inst, prob); });
     }
     return make_warmup(nullptr, QueensProblem(model.attr("N").cast<int>(), model.attr("G").cast<int>()));
   });
@@ -66,11 +64,10 @@ PYBIND11_MODULE(_tts_hip, m) {
       "make_pfsp_cpu_engine",
       [](int jobs, int machines, std::vector<int> p, int lb, size_t batch, int threads) -> std::unique_ptr<IEngine> {
         auto inst = std::make_shared<PfspInstance>(make_instance(jobs, machines, std::move(p)));
-        return with_pfsp_bucket(jobs, [&](auto nj) -> std::unique_ptr<IEngine> {
-          constexpr int NJ = decltype(nj)::value;
-          // LB1 is evaluated with the incremental LB1_d on the CPU (same values)
-          return std::make_unique<OwningCpuEngine<PfspProblem<NJ>>>(inst, PfspProblem<NJ>(*inst, lb == 1 ? 0 : lb),
-                                                                     batch, threads);
+        // LB1 is evaluated with the incremental LB1_d on the CPU (same values); the node
+        // layout is the GPU engines' (front nodes where they apply)
+        return with_pfsp_problem(*inst, lb == 1 ? 0 : lb, [&](auto prob) -> std::unique_ptr<IEngine> {
+          return std::make_unique<OwningCpuEngine<decltype(prob)>>(inst, prob, batch, threads);
         });
       },
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("batch") = 4096,

@@ -11,6 +11,7 @@
 #include <type_traits>
 #include <utility>
 
+#include "pfsp_front.hpp"
 #include "report.hpp"
 
 namespace tts {
@@ -72,9 +73,7 @@ RunResult run_multicore(const Problem& prob, int best_init, const MulticoreConfi
 
 inline RunResult run_pfsp_cpu(const PfspInstance& in, int lb, int best_init, int threads, const MulticoreConfig& cfg,
                               bool verbose) {
-  return with_pfsp_bucket(in.jobs, [&](auto nj) {
-    constexpr int NJ = decltype(nj)::value;
-    PfspProblem<NJ> prob(in, lb);
+  return with_pfsp_problem(in, lb, [&](auto prob) {
     if (threads <= 0) return run_sequential(prob, best_init);
     MulticoreConfig c = cfg;
     c.threads = threads;

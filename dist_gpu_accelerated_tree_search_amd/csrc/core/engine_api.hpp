@@ -28,17 +28,6 @@ struct EngineConfig {
   int iters_first = 18;                  // first replay after begin(): covers a 20-job tree in one graph
   int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
   int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
-  int narrow_bp = 16;                    // narrow local DFS for windows of <= this many parents per workgroup
-  int narrow_steps = 0;                  // ... up to this many steps per chunk (<= 1: off; measured slower)
-  int narrow_cap = 512;                  // ... while the chunk's stack holds <= this many nodes
-  // persistent iterations (kernels that have them): a pool of at least persist_min parents
-  // is searched to the end inside one kernel by persist_wg workgroups sharing work.
-  // Off by default: measured slower than level-per-kernel iterations on every tree tried
-  // (profiles/r2/persist.md); TTS_PERSIST_MIN turns it on.
-  size_t persist_min = 0;                // 0: off
-  int persist_us = 2000;                 // budget of one persistent iteration
-  int persist_wg = 0;                    // 0: min(grid, parent-window chunks / 2)
-  int persist_dmin = 64;                 // a donor splits stacks of at least this many nodes
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };
@@ -50,10 +39,6 @@ struct EngineStats {
   size_t pinned_bytes = 0;  // pinned host spill blocks held
   double t_run = 0, t_memcpy = 0, t_malloc = 0;
   size_t device_nodes = 0, host_nodes = 0, capacity = 0;
-  // persistent iterations (cumulative since the engine was made): workgroup steps,
-  // donations between workgroups, idle waits, microseconds spent waiting (summed)
-  unsigned long long p_steps = 0, p_donations = 0, p_waits = 0;
-  double p_wait_us = 0;
 };
 
 // Type-erased interface used by the Python bindings and the native CLIs.

@@ -56,6 +56,28 @@ TTS_HD inline PfspNode<NJ> pfsp_child(const PfspNode<NJ>& parent, int k) {
   return c;
 }
 
+// Front-carrying node of the LB1 / LB1_d search on small instances (<= 32 jobs,
+// machine bucket MB in {5, 10, 20}). LB1 only depends on the scheduled prefix through
+// its per-machine completion times (front) and on the set of unscheduled jobs, so the
+// node stores exactly that: a child costs O(M) from its parent instead of replaying
+// the O(depth * M) prefix chain (ref schedule_front, c_bound_simple.c:52-69, which
+// the reference repeats per child for LB1 and per parent for LB1_d). 32 B for up to
+// 10 machines, 48 B for 20 (the permutation node is 32 B at 20 jobs).
+//   depth       jobs scheduled
+//   rest        bit j set: job j is not scheduled yet
+//   front[m]    completion time of the prefix on machine m; at the root the minimum
+//               heads (ref schedule_front with limit1 == -1)
+template <int MB>
+struct alignas(16) PfspFrontNode {
+  static constexpr int kMachines = MB;
+  uint8_t depth;
+  uint8_t pad[3];
+  uint32_t rest;
+  uint16_t front[MB];
+};
+static_assert(sizeof(PfspFrontNode<5>) == 32 && sizeof(PfspFrontNode<10>) == 32 && sizeof(PfspFrontNode<20>) == 48,
+              "front node sizes");
+
 // Job-count buckets a run-time instance is dispatched to.
 inline int pfsp_bucket(int jobs) {
   if (jobs <= 20) return 20;

@@ -112,19 +112,12 @@ class DeviceEngine final : public IEngine {
     if (const char* f = std::getenv("TTS_LOCAL_STEPS")) pa.local_steps = std::min(std::max(0, std::atoi(f)), Traits::kLocalSteps);
     pa.local_min = 0;
     if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
-    pa.narrow_bp = cfg_.narrow_bp;
-    pa.narrow_steps = std::min(cfg_.narrow_steps, Traits::kLocalSteps > 1 ? 64 : 0);
-    pa.narrow_cap = cfg_.narrow_cap;
-    if (const char* f = std::getenv("TTS_NARROW_BP")) pa.narrow_bp = std::max(0, std::atoi(f));
-    if (const char* f = std::getenv("TTS_NARROW_STEPS")) pa.narrow_steps = std::max(0, std::atoi(f));
-    if (const char* f = std::getenv("TTS_NARROW_CAP")) pa.narrow_cap = std::max(0, std::atoi(f));
     int cus = 0;
     TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
     cus_ = cus;
     int per_cu = std::max(1, Traits::blocks_per_cu());
     if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(g));  // tuning
     grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, static_cast<size_t>(cus) * per_cu)));
-    setup_persist();
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known
     // pool spans a whole parent window (spec_min_). Queuing it earlier
@@ -173,7 +166,6 @@ class DeviceEngine final : public IEngine {
       (void)hipFree(d_cnt_[b]);
       (void)hipFree(d_lcnt_[b]);
     }
-    if (args_.pool.pws) (void)hipFree(args_.pool.pws);
     (void)hipFree(d_ctl_);
     (void)hipHostFree(h_ctl_);
     (void)hipHostFree(h_up_);
@@ -415,8 +407,6 @@ class DeviceEngine final : public IEngine {
     h_ctl_->split_world = arm_world_ > 1 ? arm_world_ : 0;
     h_ctl_->split_rank = arm_rank_;
     h_ctl_->split_min = arm_min_;
-    h_ctl_->perr = 0;
-    reset_persist();
     for (int i = 0; i < 3; ++i) h_ctl_->slot[i].sdone = 0;
     const bool armed = arm_world_ > 1;
     arm_world_ = 0;
@@ -430,9 +420,7 @@ class DeviceEngine final : public IEngine {
       return;
     }
     h_ctl_->tree = h_ctl_->sol = h_ctl_->parents = h_ctl_->iters = 0;
-    for (auto& x : h_ctl_->pend_p) x = 0;
     for (auto& x : h_ctl_->xacc) x.tree = x.sol = 0;
-    for (auto& sl : h_ctl_->slot) sl.pers = 0;
     h_ctl_->best.v = best;
     h_ctl_->bot = 0;
     h_ctl_->slot[0].stack = 0;
@@ -474,7 +462,6 @@ class DeviceEngine final : public IEngine {
       const size_t total = dev_total();
       if (total == 0 || total + 7 * buf_nodes_ > cap_) break;
       auto a = args_;
-      a.pool.persist_min = 0;  // identical iterations on every rank
       a.pool.max_parents = static_cast<int>(win);
       a.pool.max_chunks = static_cast<int>((win + Traits::kParentsPerChunk - 1) / Traits::kParentsPerChunk);
       const int m = next_mirror_;
@@ -558,8 +545,8 @@ class DeviceEngine final : public IEngine {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();
     EngineStats s = stats_;
-    s.tree = h_ctl_->tree + h_ctl_->pend_children + h_ctl_->pend_internal + h_ctl_->pend_p[0];
-    s.sol = h_ctl_->sol + h_ctl_->pend_leaves + h_ctl_->pend_p[1];
+    s.tree = h_ctl_->tree + h_ctl_->pend_children + h_ctl_->pend_internal;
+    s.sol = h_ctl_->sol + h_ctl_->pend_leaves;
     for (const auto& x : h_ctl_->xacc) {
       s.tree += x.tree;
       s.sol += x.sol;
@@ -574,11 +561,6 @@ class DeviceEngine final : public IEngine {
     s.host_nodes = spill_.size() + refill_n_;
     s.capacity = cap_;
     s.pinned_bytes = spill_.pinned_bytes();
-    s.p_steps = h_ctl_->pdiag[0] + h_ctl_->pend_p[2];
-    s.p_donations = h_ctl_->pdiag[1] + h_ctl_->pend_p[3];
-    s.p_waits = h_ctl_->pdiag[2] + h_ctl_->pend_p[4];
-    s.p_wait_us = static_cast<double>(h_ctl_->pdiag[3] + h_ctl_->pend_p[5]) * 1000.0 /
-                  static_cast<double>(std::max(1, wall_khz_));
     return s;
   }
   void synchronize() override {
@@ -588,11 +570,6 @@ class DeviceEngine final : public IEngine {
 
  private:
   void check_overflow() {
-    if (h_ctl_->perr) {
-      persist_dirty_ = true;
-      throw std::runtime_error("persistent iteration: work-sharing watchdog expired (code " +
-                               std::to_string(h_ctl_->perr) + ")");
-    }
     if (h_ctl_->overflow == 2)
       throw std::runtime_error("pool outgrew the parent window before the armed rank split (set_split)");
     if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
@@ -668,15 +645,6 @@ class DeviceEngine final : public IEngine {
   // Host shadow must be current (sync_ctl); between graph replays slot 0 is active
   // and the latest children are in buffer phase_ & 1 (graphs of 3k iterations).
   void normalize() {
-    // counts of a persistent last iteration join the plain counters (the next
-    // iteration must not fold them again)
-    if (h_ctl_->slot[0].pers) {
-      h_ctl_->tree += h_ctl_->pend_p[0];
-      h_ctl_->sol += h_ctl_->pend_p[1];
-      for (int k = 0; k < 4; ++k) h_ctl_->pdiag[k] += h_ctl_->pend_p[2 + k];
-      h_ctl_->slot[0].pers = 0;
-    }
-    for (auto& x : h_ctl_->pend_p) x = 0;
     // subtrees finished inside iterations (N-Queens)
     for (auto& x : h_ctl_->xacc) {
       h_ctl_->tree += x.tree;
@@ -723,68 +691,6 @@ class DeviceEngine final : public IEngine {
     if (kind != hipMemcpyDeviceToDevice) TTS_HIP_CHECK(hipStreamSynchronize(stream_));
     h_ctl_->bot = (h_ctl_->bot + n) & (cap_ - 1);
     h_ctl_->slot[0].stack -= n;
-  }
-
-  // Persistent iterations (kernels with Traits::kPersist): persist_wg workgroups, each
-  // with persist_r chunk slots of the children buffer as its stack; off when the parent
-  // window has too few chunks for a useful grid. TTS_PERSIST_MIN / _US / _WG / _DMIN
-  // override the configuration (A/B runs).
-  void setup_persist() {
-    auto& pa = args_.pool;
-    pa.persist_min = 0;
-    pa.pws = nullptr;
-    if (!Traits::kPersist) return;
-    size_t pmin = cfg_.persist_min;
-    int us = cfg_.persist_us, wg = cfg_.persist_wg, dmin = cfg_.persist_dmin;
-    if (const char* f = std::getenv("TTS_PERSIST_MIN")) pmin = static_cast<size_t>(std::max(0L, std::atol(f)));
-    if (const char* f = std::getenv("TTS_PERSIST_US")) us = std::max(1, std::atoi(f));
-    if (const char* f = std::getenv("TTS_PERSIST_WG")) wg = std::max(0, std::atoi(f));
-    if (const char* f = std::getenv("TTS_PERSIST_DMIN")) dmin = std::max(2, std::atoi(f));
-    grid_p_ = static_cast<int>(std::min<size_t>(max_chunks_, static_cast<size_t>(cus_) *
-                                                             static_cast<size_t>(std::max(1, Traits::blocks_per_cu_persist()))));
-    int P = wg > 0 ? wg : static_cast<int>(max_chunks_ / 2);
-    P = std::min({P, grid_p_, static_cast<int>(max_chunks_)});
-    if (pmin == 0 || P < 64) return;
-    const int R = static_cast<int>(max_chunks_ / P);
-    int khz = 0;
-    TTS_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device));
-    if (khz <= 0) khz = 100000;
-    wall_khz_ = khz;
-    const size_t ws_bytes = 2 * sizeof(dev::PersistWs);
-    const size_t box_bytes = static_cast<size_t>(P) * sizeof(dev::PersistBox);
-    const size_t pst_bytes = 2 * static_cast<size_t>(P) * dev::kPstWords * sizeof(dev::u64);
-    char* mem = nullptr;
-    const size_t bytes = ws_bytes + box_bytes + pst_bytes;
-    TTS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&mem), bytes));
-    TTS_HIP_CHECK(hipMemset(mem, 0, bytes));
-    pa.pws = reinterpret_cast<dev::PersistWs*>(mem);
-    pa.box = reinterpret_cast<dev::PersistBox*>(mem + ws_bytes);
-    pa.pst = reinterpret_cast<dev::u64*>(mem + ws_bytes + box_bytes);
-    persist_bytes_ = bytes;
-    // a persistent iteration explores a 20-job tree right after begin(): a short first
-    // replay (its empty tail iterations cost ~4.5 us each)
-    cfg_.iters_first = 6;
-    pa.persist_min = pmin;
-    pa.persist_ticks = static_cast<dev::u64>(us) * static_cast<dev::u64>(khz) / 1000;
-    pa.persist_wg = P;
-    pa.persist_r = R;
-    pa.persist_dmin = std::max(2, dmin);
-    pa.persist_wt = 1;
-    if (const char* f = std::getenv("TTS_PERSIST_WT")) pa.persist_wt = std::atoi(f) != 0;
-    persist_ = true;
-  }
-  // one iteration: the kernel with persistent iterations when they are on
-  void launch_iter(const Args& a, int t, hipStream_t s) const {
-    if (persist_)
-      Traits::launch_persist(a, t, grid_p_, s);
-    else
-      Traits::launch(a, t, grid_, s);
-  }
-  // After a watchdog error the generation words may be inconsistent: start clean.
-  void reset_persist() {
-    if (!persist_dirty_ || !args_.pool.pws) return;
-    TTS_HIP_CHECK(hipMemsetAsync(args_.pool.pws, 0, persist_bytes_, stream_));
-    persist_dirty_ = false;
   }
 
   // Pinned spill blocks: 1/16 of the ring, between 64K nodes and 256 MB.
@@ -924,7 +830,7 @@ class DeviceEngine final : public IEngine {
       hipGraphExec_t g = K > 0 ? first_graph(K)[m] : graphs_[phase_ / 3][m][gi];
       TTS_HIP_CHECK(hipGraphLaunch(g, stream_));
     } else {
-      for (int i = 0; i < k; ++i) launch_iter(args_, (phase_ + i) % 6, stream_);
+      for (int i = 0; i < k; ++i) Traits::launch(args_, (phase_ + i) % 6, grid_, stream_);
       auto pa = args_.pool;
       pa.mirror = d_mirror_[m];
       Traits::finalize(pa, ((phase_ + k) % 6) & 1, stream_);
@@ -957,7 +863,7 @@ class DeviceEngine final : public IEngine {
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     hipGraph_t g;
     TTS_HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < K; ++i) launch_iter(args_, (phase + i) % 6, cs);
+    for (int i = 0; i < K; ++i) Traits::launch(args_, (phase + i) % 6, grid_, cs);
     auto pa = args_.pool;
     pa.mirror = d_mirror_[mirror];
     Traits::finalize(pa, ((phase + K) % 6) & 1, cs);
@@ -1001,11 +907,6 @@ class DeviceEngine final : public IEngine {
   dev::u64 launched_seq_ = 0;  // finalize kernels enqueued (== device ctl->seq when idle)
   bool poll_ = true;           // spin on the mirror's sequence word (TTS_POLL=0: event sync)
   bool fresh_ = false;         // no graph launched since begin()
-  bool persist_ = false;       // graphs of the kernel with persistent iterations (setup_persist)
-  int grid_p_ = 0;             // its grid
-  int wall_khz_ = 100000;      // device wall clock (s_memrealtime) rate
-  bool persist_dirty_ = false; // a persistent iteration's watchdog fired: clear its state at begin()
-  size_t persist_bytes_ = 0;
   int arm_world_ = 0, arm_rank_ = 0;  // split armed for the next begin() (set_split)
   size_t arm_min_ = 1;
   hipStream_t stream_ = nullptr, own_stream_ = nullptr;

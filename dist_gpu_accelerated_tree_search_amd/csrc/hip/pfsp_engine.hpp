@@ -16,8 +16,10 @@
 #include <vector>
 
 #include "../core/pfsp_bounds_cpu.hpp"
+#include "../core/pfsp_front.hpp"
 #include "../core/pfsp_instance.hpp"
 #include "engine.hpp"
+#include "pfsp_front_kernels.hpp"
 #include "pfsp_kernels.hpp"
 
 namespace tts {
@@ -31,23 +33,9 @@ struct PfspTraits {
   static constexpr int kChildrenPerChunk = G::SLOT;  // slot region per chunk
   static constexpr int kMaxChildren = NJ;            // children per parent (one level)
   static constexpr int kLocalSteps = G::LT;
-  static constexpr bool kPersist = G::LT > 1;  // persistent iterations (the LB1 register path)
   static constexpr int kMaxChunks = G::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
-  }
-  // the kernel with persistent iterations (kPersist only)
-  static void launch_persist(const Args& a, int t, int grid, hipStream_t s) {
-    if constexpr (kPersist)
-      hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK, true>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
-  }
-  static int blocks_per_cu_persist() {
-    int n = 0;
-    if constexpr (kPersist)
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_expand_kernel<NJ, M, LBK, true>, dev::kBlock, 0) !=
-          hipSuccess)
-        return 1;
-    return n;
   }
   static void flatten(const dev::PoolArgs<Node>& pa, int b, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::SLOT, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
@@ -64,6 +52,50 @@ struct PfspTraits {
     return n;
   }
 };
+
+// LB1 / LB1_d on front-carrying nodes (pfsp_front_kernels.hpp), machine bucket M.
+template <int M>
+struct PfspFrontTraits {
+  using Node = PfspFrontNode<M>;
+  using Args = dev::PfspFrontArgs<M>;
+  using G = dev::FrontGeom<M>;
+  static constexpr int kParentsPerChunk = G::BP;
+  static constexpr int kChildrenPerChunk = G::SLOT;
+  static constexpr int kMaxChildren = G::NJ;
+  static constexpr int kLocalSteps = G::LT;
+  static constexpr int kMaxChunks = G::MAXCHUNKS;
+  static void launch(const Args& a, int t, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
+  }
+  static void flatten(const dev::PoolArgs<Node>& pa, int b, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::SLOT, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
+                       pa, b);
+  }
+  static void finalize(const dev::PoolArgs<Node>& pa, int b, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, G::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa, b);
+  }
+  static int blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_front_kernel<M>, dev::kBlock, 0) != hipSuccess)
+      return 1;
+    return n;
+  }
+};
+
+// Front-layout tables: job-major u16 p rows padded to the LDS stride, padded tails.
+template <int M>
+inline std::vector<uint16_t> pfsp_front_fill_args(const PfspInstance& in, dev::PfspFrontArgs<M>& a) {
+  if (!pfsp_front_ok(in, 1) || pfsp_machine_bucket(in.machines) != M)
+    throw std::invalid_argument("front layout does not apply to this instance");
+  constexpr int MS = dev::FrontGeom<M>::MS;
+  const PfspPadded t = pfsp_padded_tables(in, M);
+  std::vector<uint16_t> ptab(static_cast<size_t>(in.jobs) * MS, 0);
+  for (int j = 0; j < in.jobs; ++j)
+    for (int m = 0; m < in.machines; ++m) ptab[static_cast<size_t>(j) * MS + m] = static_cast<uint16_t>(in.pt(m, j));
+  a.jobs = in.jobs;
+  for (int m = 0; m < M; ++m) a.min_tails[m] = t.tails[m];
+  return ptab;
+}
 
 // Host-side images of the device tables.
 struct PfspTableImages {
@@ -175,10 +207,6 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
   a.npairs = PR;
   a.rs4 = img.rs4;
   a.lb2_pipe = lb2_pipe_wanted();
-  // last-level finishing: ta008 LB1_d 5.62 -> 5.45 ms, ta014 LB1 0.296 -> 0.30 ms
-  // (profiles/r2/lb1_fin.txt): off by default, TTS_LB1_FIN=1 turns it on
-  a.lb1_fin = 0;
-  if (const char* f = std::getenv("TTS_LB1_FIN")) a.lb1_fin = std::atoi(f) != 0;
   a.lb2_dyn = lb2_dyn_wanted();
   a.lb2_stride = lb2_stride_wanted();
   for (int m = 0; m < M; ++m) {
@@ -455,6 +483,61 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
   }
 }
 
+template <int M>
+std::unique_ptr<IEngine> make_pfsp_front_engine_t(const PfspInstance& in, const EngineConfig& cfg) {
+  TTS_HIP_CHECK(hipSetDevice(cfg.device));
+  dev::PfspFrontArgs<M> a{};
+  const std::vector<uint16_t> ptab = pfsp_front_fill_args(in, a);
+  a.ptab = upload_vec(ptab);
+  auto eng = std::make_unique<DeviceEngine<PfspFrontTraits<M>>>(cfg, a);
+  eng->adopt(const_cast<uint16_t*>(a.ptab));
+  return eng;
+}
+
+// Bounds of permutation-layout parents through the front kernel (tests): parents are
+// converted on the host, bounds come back in the permutation's child order k = depth..N-1.
+template <int M>
+std::vector<int> pfsp_front_bounds_t(const PfspInstance& in, const PfspNode<20>* ph, size_t n, int device) {
+  using FNode = PfspFrontNode<M>;
+  TTS_HIP_CHECK(hipSetDevice(device));
+  const PfspFrontProblem<M> prob(in, 1);
+  std::vector<FNode> fn(n);
+  std::vector<int> offsets(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    fn[i] = pfsp_front_from_perm(prob, ph[i]);
+    offsets[i + 1] = offsets[i] + (in.jobs - ph[i].depth);
+  }
+  const size_t nb = static_cast<size_t>(offsets[n]);
+  std::vector<int> by_job(nb, 0), out(nb, 0);
+  if (n == 0) return out;
+  dev::PfspFrontArgs<M> a{};
+  const std::vector<uint16_t> ptab = pfsp_front_fill_args(in, a);
+  a.ptab = upload_vec(ptab);
+  a.offsets = upload_vec(offsets);
+  a.parents_in = upload_vec(fn);
+  int* dbounds = nullptr;
+  TTS_HIP_CHECK(hipMalloc(&dbounds, std::max<size_t>(1, nb) * sizeof(int)));
+  a.bounds_out = dbounds;
+  a.nparents = static_cast<int>(n);
+  const int blocks = static_cast<int>(std::min<size_t>((n + dev::kBlock - 1) / dev::kBlock, 2048));
+  hipLaunchKernelGGL((dev::pfsp_front_bounds_kernel<M>), dim3(blocks), dim3(dev::kBlock), 0, 0, a);
+  TTS_HIP_CHECK(hipGetLastError());
+  TTS_HIP_CHECK(hipDeviceSynchronize());
+  TTS_HIP_CHECK(hipMemcpy(by_job.data(), dbounds, nb * sizeof(int), hipMemcpyDeviceToHost));
+  (void)hipFree(dbounds);
+  (void)hipFree(const_cast<int*>(a.offsets));
+  (void)hipFree(const_cast<FNode*>(a.parents_in));
+  (void)hipFree(const_cast<uint16_t*>(a.ptab));
+  for (size_t i = 0; i < n; ++i) {
+    const int d = ph[i].depth;
+    for (int k = d; k < in.jobs; ++k) {
+      const int job = ph[i].prmu[k];
+      out[offsets[i] + (k - d)] = by_job[offsets[i] + __builtin_popcount(fn[i].rest & ((1u << job) - 1u))];
+    }
+  }
+  return out;
+}
+
 // Kernel machine bucket: 5, 10 or 20 (Taillard's counts); other counts up to 20 run
 // in the next bucket with zero-time padding machines (pfsp_fill_args).
 template <class F>
@@ -489,6 +572,8 @@ TTS_PFSP_DECLARE_BUCKET(500)
   std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg) { \
     return with_machine_bucket(in.machines, [&](auto mm) -> std::unique_ptr<IEngine> {               \
       constexpr int M = decltype(mm)::value;                                                         \
+      if constexpr (NJ == 20)                                                                        \
+        if (pfsp_front_ok(in, lb)) return make_pfsp_front_engine_t<M>(in, cfg);                      \
       if (lb != 2) return make_pfsp_engine_t<NJ, M, 1>(in, cfg);                                    \
       if constexpr (NJ == 50)                                                                        \
         if (lb2_pack_wanted(in)) return make_pfsp_engine_t<NJ, M, 3>(in, cfg);                       \
@@ -502,6 +587,9 @@ TTS_PFSP_DECLARE_BUCKET(500)
                                           int device) {                                              \
     return with_machine_bucket(in.machines, [&](auto mm) {                                           \
       constexpr int M = decltype(mm)::value;                                                         \
+      if constexpr (NJ == 20)                                                                        \
+        if (pfsp_front_ok(in, lb))                                                                   \
+          return pfsp_front_bounds_t<M>(in, static_cast<const PfspNode<20>*>(parents), n, device);   \
       return lb == 2 ? pfsp_gpu_bounds_t<NJ, M, 2>(in, parents, n, best, device)                    \
                      : pfsp_gpu_bounds_t<NJ, M, 1>(in, parents, n, best, device);                   \
     });                                                                                              \

@@ -121,9 +121,6 @@ struct PfspArgs {
   // per-workgroup timeline (probe only): wall clock (s_memrealtime) at entry, after
   // the iteration prologue, and at exit, 3 values per workgroup
   unsigned long long* dbg_blk;
-  // one-level LB1 loop: parents with two jobs left evaluate their children's complete
-  // schedules in place (lb1_small_parent FIN; TTS_LB1_FIN=1: on)
-  int lb1_fin;
 };
 
 template <int NJ, int M, int LBK>
@@ -444,7 +441,7 @@ template <int NJ, int M, class Smem, class Emit>
 __device__ inline void pfsp_lb1_parent(const PfspArgs<NJ, M>& a, Smem& sm, int p, Emit emit) {
   const PfspNode<NJ>& nd = sm.node[p];
   const int d = nd.depth;
-  int f[M], r[M];  // r: unscheduled work + min tail (see lb1_small_parent)
+  int f[M], r[M];  // r: unscheduled work + min tail, folded in once per parent
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     f[m] = (d == 0) ? a.min_heads[m] : 0;
@@ -484,8 +481,6 @@ __device__ inline void pfsp_lb1_parent(const PfspArgs<NJ, M>& a, Smem& sm, int p
 // state slot t%3, buffer parity t%2.
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
-template <int NJ, int M, bool PK = false>
-__device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t);
 
 template <int NJ, int M, bool PACK, bool PS, bool PK = false>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
@@ -495,13 +490,8 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 // spills); LB2 is bounded by its LDS footprint instead (4 workgroups per CU for
 // 50 x 20), and the packed-walk kernel (LBK 5) is held to the 128 VGPRs of 4 waves
 // per SIMD (its unrolled walk would otherwise take 130).
-//
-// PK: the same kernel with persistent iterations compiled in (lb1_small_persist, the
-// LB1 register path only), held to 4 waves per SIMD (128 VGPRs): its work-sharing loop
-// does not fit the plain kernel's budget without spills, and the persistent grid is 4
-// workgroups per CU anyway. The engine replays graphs of it when persistence is on.
-template <int NJ, int M, int LBK, bool PK = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PK ? 4 : LBK == 5 ? 4 : LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
+template <int NJ, int M, int LBK>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK == 5 ? 4 : LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
 void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
     pfsp_expand_lb2<NJ, M, false, false>(a, t);
@@ -513,10 +503,8 @@ void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
     pfsp_expand_lb2<NJ, M, false, false, true>(a, t);  // two children per lane, packed u16 walks
   else if constexpr (LBK == 5)
     pfsp_expand_lb2<NJ, M, false, false>(a, t);  // (job sets of one word only)
-  else if constexpr (sizeof(PfspNode<NJ>) == 32)
-    pfsp_expand_lb1_small<NJ, M, PK>(a, t);
   else
-    pfsp_expand_lb1<NJ, M>(a, t);
+    pfsp_expand_lb1<NJ, M>(a, t);  // permutation nodes (20-job instances use pfsp_front_kernels.hpp)
 }
 
 // ---------------------------------------------------------------------------
@@ -1259,796 +1247,6 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// 20-job bucket (NJ <= 32, 32-B nodes): the parent node lives in 8 registers. The
-// prefix and children loops are unrolled over all NJ positions and predicated on
-// the depth, so every job id is extracted with a static shift (v_bfe) — no LDS
-// node reads at all (the previous LDS node rows were read byte-wise by 64 lanes
-// with a 32-B stride: 8-way bank conflicts, profiles/r1/r1_pmc). The only LDS
-// traffic is one padded p-table row per scheduled job and per child.
-template <int NJ>
-__device__ inline uint32_t node_byte(const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], int e) {
-  constexpr int NWD = sizeof(PfspNode<NJ>) / 4;
-  uint32_t x = 0;
-#pragma unroll
-  for (int i = 0; i < NWD; ++i) x = (i == (e >> 2)) ? w[i] : x;
-  return (x >> ((e & 3) * 8)) & 0xffu;
-}
-
-template <int NJ, int M>
-struct PfspSmemLB1s {
-  using G = PfspGeom<NJ, 1>;
-  // two-level iterations: parents per chunk such that their children fit one per
-  // thread and their grandchildren fit the chunk's MAXCH slots
-  static constexpr int BPF = (kBlock / NJ) < (G::MAXCH / (NJ * (NJ - 1))) ? (kBlock / NJ) : (G::MAXCH / (NJ * (NJ - 1)));
-  uint16_t ptab[NJ][PfspConsts<M>::MS];
-  int scan[kBlock / kWave];
-  uint4 mid[kBlock][2];  // level-1 survivors of a two-level chunk
-  PoolSmem<G::MAXCHUNKS> pool;
-  int bc[12];            // persistent iterations: thread 0 -> workgroup broadcasts, thread 0 state
-  u64 bq;
-  u64 dl[3];             // persistent iterations: budget deadline, watchdog deadline, ticks waited (thread 0)
-};
-
-// Bounds of every child of the parent held in w (valid lanes only); calls
-// emit(k, lb) for each child position k (static after unrolling).
-//
-// FIN (the one-level loop, a.lb1_fin): a parent with two jobs left hands its children to
-// fin(k, lb, leaf_lb) instead: the child's bound and the bound of its single child, the
-// complete schedule (what the next iteration would compute with the child as parent), so
-// the last tree level never goes through the pool.
-struct NoFin {
-  __device__ void operator()(int, int, int) const {}
-};
-template <int NJ, int M, bool FIN = false, class Emit, class Fin = NoFin>
-__device__ inline void lb1_small_parent(const PfspArgs<NJ, M>& a, const PfspSmemLB1s<NJ, M>& sm,
-                                        const uint32_t (&w)[sizeof(PfspNode<NJ>) / 4], Emit emit,
-                                        Fin fin = Fin{}) {
-  const auto& ptab = sm.ptab;
-  const int d = static_cast<int>(w[0] & 0xffu);
-  // r[m] = unscheduled work on machine m + its min tail: the tail is folded in
-  // once per parent instead of once per child and machine
-  int f[M], r[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    f[m] = (d == 0) ? a.min_heads[m] : 0;
-    r[m] = a.sum_all[m] + a.min_tails[m];
-  }
-#pragma unroll
-  for (int i = 0; i < NJ - 1; ++i) {
-    if (i < d) {
-      const int job = static_cast<int>((w[(1 + i) >> 2] >> (((1 + i) & 3) * 8)) & 0xffu);
-      int pr[M];
-      load_prow<M>(ptab[job], pr);
-      f[0] += pr[0];
-      r[0] -= pr[0];
-#pragma unroll
-      for (int m = 1; m < M; ++m) {
-        f[m] = max(f[m - 1], f[m]) + pr[m];
-        r[m] -= pr[m];
-      }
-    }
-  }
-  const bool pre = FIN && a.lb1_fin && d + 2 == a.jobs;
-#pragma unroll
-  for (int k = 0; k < NJ; ++k) {
-    if (k >= d && k < a.jobs && !pre) {
-      const int job = static_cast<int>((w[(1 + k) >> 2] >> (((1 + k) & 3) * 8)) & 0xffu);
-      int pr[M];
-      load_prow<M>(ptab[job], pr);
-      int lb = f[0] + r[0];
-      int tt = f[0] + pr[0];
-#pragma unroll
-      for (int m = 1; m < M; ++m) {
-        const int sv = max(tt, f[m]);
-        lb = max(lb, sv + r[m]);
-        tt = sv + pr[m];
-      }
-      emit(k, lb);
-    }
-  }
-  if constexpr (FIN) {
-    if (pre) {
-#pragma unroll 1
-      for (int q = 0; q < 2; ++q) {
-        const int k = d + q, o = d + 1 - q;  // the child's job position and the last job's
-        const int jk = static_cast<int>(node_byte<NJ>(w, 1 + k)), jo = static_cast<int>(node_byte<NJ>(w, 1 + o));
-        int pk[M], po[M], fc[M];
-        load_prow<M>(ptab[jk], pk);
-        load_prow<M>(ptab[jo], po);
-        int lb = f[0] + r[0];
-        int tt = f[0] + pk[0];
-        fc[0] = tt;
-#pragma unroll
-        for (int m = 1; m < M; ++m) {
-          const int sv = max(tt, f[m]);
-          lb = max(lb, sv + r[m]);
-          tt = sv + pk[m];
-          fc[m] = tt;
-        }
-        // the complete schedule: the child as parent (remain r - pk), the last job
-        int lbl = fc[0] + r[0] - pk[0];
-        int t2 = fc[0] + po[0];
-#pragma unroll
-        for (int m = 1; m < M; ++m) {
-          const int sv = max(t2, fc[m]);
-          lbl = max(lbl, sv + r[m] - pk[m]);
-          t2 = sv + po[m];
-        }
-        fin(k, lb, lbl);
-      }
-    }
-  }
-}
-
-__device__ inline void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// One 32-B node store, plain or write-through (8-B agent-scope stores = sc1: the line
-// leaves this XCD's L2, so a later writer on another XCD is never shadowed by it).
-__device__ inline void st_node(uint4* dst, const uint4& x0, const uint4& x1, bool wt) {
-  if (wt) {
-    u64* d = reinterpret_cast<u64*>(dst);
-    __hip_atomic_store(d + 0, (static_cast<u64>(x0.y) << 32) | x0.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(d + 1, (static_cast<u64>(x0.w) << 32) | x0.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(d + 2, (static_cast<u64>(x1.y) << 32) | x1.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(d + 3, (static_cast<u64>(x1.w) << 32) | x1.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    dst[0] = x0;
-    dst[1] = x1;
-  }
-}
-__device__ inline u64 uni64(u64 x) {
-  const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(x));
-  const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(x >> 32));
-  return (static_cast<u64>(hi) << 32) | lo;
-}
-
-// Children of the parent held in w whose positions are set in surv, written as
-// consecutive 32-B nodes from dst (node words in registers, element 0 = depth).
-template <int NJ>
-__device__ inline void emit_children(const uint32_t (&w)[8], uint32_t surv, uint4* dst, bool wt = false) {
-  const int d = static_cast<int>(w[0] & 0xffu);
-  const uint32_t jd = node_byte<NJ>(w, 1 + d);
-  uint32_t base[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) base[i] = w[i];
-  base[0] = (base[0] & ~0xffu) | static_cast<uint32_t>(d + 1);
-  while (surv) {
-    const int k = __ffs(surv) - 1;
-    surv &= surv - 1;
-    uint32_t c[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) c[i] = base[i];
-    node_set<NJ>(c, 1 + d, node_byte<NJ>(w, 1 + k));
-    node_set<NJ>(c, 1 + k, jd);
-    const uint4 x0 = make_uint4(c[0], c[1], c[2], c[3]), x1 = make_uint4(c[4], c[5], c[6], c[7]);
-    if (wt) {
-      st_node(dst, x0, x1, true);
-    } else {
-      dst[0] = x0;
-      dst[1] = x1;
-    }
-    dst += 2;
-  }
-}
-
-// Two-level chunk loop (v.fused): BPF parents per chunk, one per thread of the
-// first wave, expanded into LDS (level 1: survivors are pushed-and-popped tree
-// nodes, counted in the chunk's leaf word), then every level-1 survivor — one per
-// thread — is expanded and its survivors go to the chunk's slot region. Same
-// counting rules as the one-level loop: leaves at either level lower the
-// incumbent and count as solutions.
-template <int NJ, int M>
-__device__ inline void lb1_small_two_level(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ, M>& sm, const IterView& v,
-                                           int t, int best) {
-  using G = PfspGeom<NJ, 1>;
-  using Node = PfspNode<NJ>;
-  constexpr int BPF = PfspSmemLB1s<NJ, M>::BPF;
-  const int tid = threadIdx.x;
-  const auto& pa = a.pool;
-  Node* const bout = pa.buf[(t & 1) ^ 1];
-  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
-  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
-    uint32_t w[8];
-    const u64 gi = static_cast<u64>(ch) * BPF + tid;
-    const bool valid = tid < BPF && gi < v.B;
-    if (valid) {
-      const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool));
-      const uint4 x0 = src[0], x1 = src[1];
-      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
-      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
-    }
-    uint32_t surv = 0;
-    int nsurv = 0, nleaf = 0;
-    if (valid) {
-      const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
-        if (leaf) {
-          ++nleaf;
-          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-        } else if (lb < best) {
-          ++nsurv;
-          surv |= 1u << k;
-        }
-      });
-    }
-    int tot1 = 0;
-    const int off1 = block_exclusive_scan(nsurv, sm.scan, &tot1);
-    if (surv) emit_children<NJ>(w, surv, &sm.mid[off1][0]);
-    __syncthreads();
-    surv = 0;
-    nsurv = 0;
-    if (tid < tot1) {
-      const uint4 x0 = sm.mid[tid][0], x1 = sm.mid[tid][1];
-      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
-      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
-      const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
-        if (leaf) {
-          ++nleaf;
-          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-        } else if (lb < best) {
-          ++nsurv;
-          surv |= 1u << k;
-        }
-      });
-    }
-    int tot = 0;
-    const int off = block_exclusive_scan(nsurv | (nleaf << 16), sm.scan, &tot) & 0xffff;
-    if (tid == 0) {
-      cnt_out[ch] = tot & 0xffff;
-      lcnt_out[ch] = (tot >> 16) | (tot1 << 16);
-    }
-    if (surv) emit_children<NJ>(w, surv, reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off));
-  }
-}
-
-// Local DFS chunk loop (v.local): chunk ch takes v.bp window parents, then keeps
-// popping up to kBlock nodes from the top of its own slot region (its private stack,
-// written by this workgroup only and read back through L2) and pushing their
-// survivors there, for up to pa.local_steps steps or until the stack is empty. The
-// stack left is the chunk's output (cnt), the nodes pushed and expanded in between
-// are explored tree nodes (high half of the leaf word). Pops read slots
-// [top - n, top) and pushes write from top - n on: every pop is in registers before
-// the scan's barrier that precedes the first push.
-template <int NJ, int M>
-__device__ inline void lb1_small_local(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ, M>& sm, const IterView& v, int t,
-                                       int best) {
-  using G = PfspGeom<NJ, 1>;
-  using Node = PfspNode<NJ>;
-  const int tid = threadIdx.x;
-  const auto& pa = a.pool;
-  Node* const bout = pa.buf[(t & 1) ^ 1];
-  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
-  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  const int steps = v.steps;
-  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
-    uint4* const stk = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
-    int top = 0, pushed = 0, nleaf = 0;
-    for (int s = 0; s < steps; ++s) {
-      uint32_t w[8];
-      bool valid;
-      if (s == 0) {
-        const u64 gi = static_cast<u64>(ch) * v.bp + tid;
-        valid = tid < v.bp && gi < v.B;
-        if (valid) {
-          const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool));
-          const uint4 x0 = src[0], x1 = src[1];
-          w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
-          w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
-        }
-      } else {
-        if (top == 0) break;  // uniform
-        const int npop = min(top, kBlock);
-        valid = tid < npop;
-        if (valid) {
-          const uint4* src = stk + 2 * (top - npop + tid);
-          const uint4 x0 = src[0], x1 = src[1];
-          w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
-          w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
-        }
-        top -= npop;
-      }
-      uint32_t surv = 0;
-      int nsurv = 0;
-      if (valid) {
-        const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-        lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
-          if (leaf) {
-            ++nleaf;
-            if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-          } else if (lb < best) {
-            ++nsurv;
-            surv |= 1u << k;
-          }
-        });
-      }
-      int tot = 0;
-      const int off = block_exclusive_scan(nsurv, sm.scan, &tot);
-      if (surv) emit_children<NJ>(w, surv, stk + 2 * (top + off));
-      top += tot;
-      pushed += tot;
-      // pushes visible to the next step's pops (workgroup scope), and room left
-      // for one more full step
-      __syncthreads();
-      if (top + kBlock * NJ > G::SLOT || top > v.cap) break;
-    }
-    int leaves = 0;
-    (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
-    if (tid == 0) {
-      cnt_out[ch] = top;
-      lcnt_out[ch] = leaves | ((pushed - top) << 16);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent iteration (v.persist, pool_device.hpp): the whole window is explored in
-// this kernel. Workgroup g < persist_wg runs a depth-first search on its own stack —
-// persist_r consecutive chunk slots of the output buffer, [bot, top) — popping up to
-// kBlock nodes per step (one per thread, bounds by lb1_small_parent) and pushing the
-// survivors on top. An empty stack takes the workgroup's next window slice (slices g,
-// g + P, g + 2P, ... of `grab` parents: no shared counter). With none left the
-// workgroup goes idle and waits for a donation: it counts itself idle in its shard,
-// posts an odd generation in box[g].want and polls box[g].mail. A workgroup holding at
-// least persist_dmin nodes probes 16 random boxes per step (issued with its pops); on an
-// odd one it claims it (CAS to even, counting the receiver busy), copies the bottom half
-// of its stack (the shallowest nodes, the largest subtrees) into the receiver's slots
-// and publishes {generation, count} in its mail. Stack writes are write-through (sc1,
-// persist_wt) so no XCD's L2 holds a dirty line of another workgroup's slots: payload,
-// every wave's vmcnt(0), barrier, flag; the receiver polls, acquires, barriers
-// (cdna_hip_programming.md G16 R1). The search ends when every started workgroup is
-// idle (a consistent snapshot of the shards), or at the budget / a full stack (stop):
-// then each workgroup's untaken slices go on its stack, and the stacks are the chunks'
-// output, exactly as a local DFS iteration leaves them. Counts go to the workgroup's
-// record pst[t & 1][g] (plain stores, no shared counter): a stack pop is an explored
-// tree node, minus the untaken slices put back (counted when they were pushed).
-__device__ inline int persist_box_gen(u64 m) { return static_cast<int>(m >> 32); }
-
-// Termination check (thread 0): two identical collects of the shards, all idle.
-__device__ inline bool persist_all_idle(const PersistWs* ws) {
-  u64 a[kPersistShards], b[kPersistShards];
-#pragma unroll
-  for (int i = 0; i < kPersistShards; ++i) a[i] = __hip_atomic_load(&ws->sh[i].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  bool idle = true;
-#pragma unroll
-  for (int i = 0; i < kPersistShards; ++i) idle &= ((a[i] >> 16) & 0xffffu) == (a[i] & 0xffffu);
-  if (!idle) return false;
-#pragma unroll
-  for (int i = 0; i < kPersistShards; ++i) b[i] = __hip_atomic_load(&ws->sh[i].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  bool same = true;
-#pragma unroll
-  for (int i = 0; i < kPersistShards; ++i) same &= a[i] == b[i];
-  return same;
-}
-
-template <int NJ, int M>
-__device__ inline void lb1_small_persist(const PfspArgs<NJ, M>& a, PfspSmemLB1s<NJ, M>& sm, const IterView& v, int t,
-                                         int best0) {
-  using G = PfspGeom<NJ, 1>;
-  using Node = PfspNode<NJ>;
-  const int tid = threadIdx.x;
-  const int lane = tid & (kWave - 1);
-  const auto& pa = a.pool;
-  const int me = blockIdx.x;
-  const int P = pa.persist_wg;
-  if (me >= P) return;
-  PersistWs* const ws = pa.pws + (t & 1);
-  PersistBox* const box = pa.box;
-  Node* const bout = pa.buf[(t & 1) ^ 1];
-  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
-  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  const int R = pa.persist_r;
-  const int cap = R * G::SLOT;
-  uint4* const stk = reinterpret_cast<uint4*>(bout + static_cast<size_t>(me) * cap);
-  const u64 B = v.B;
-  const bool wt = pa.persist_wt != 0;
-  u64* const shard = &ws->sh[me % kPersistShards].v;
-  // window slices: me, me + P, ...; room for the untaken ones is kept on the stack
-  const int grab = static_cast<int>(min(static_cast<u64>(kBlock), max(1ull, (B + P - 1) / P)));
-  const u64 nsl = (B + grab - 1) / grab;
-  u64 sl = static_cast<u64>(me);
-  const int mine = sl < nsl ? static_cast<int>((nsl - 1 - sl) / P + 1) : 0;
-  const int lim = cap - mine * grab;  // pushes stay below this
-  // thread 0's state lives in LDS (registers are the LB1 loop's): sm.bc[9] want
-  // generation (even between waits), sm.bc[11] waits, sm.dl = budget / watchdog
-  // deadlines and ticks spent waiting
-  if (tid == 0) {
-    __hip_atomic_fetch_add(shard, (1ull << 32) | (1ull << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm.bc[9] = static_cast<int>(__hip_atomic_load(&box[me].want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    sm.bc[11] = 0;
-    sm.bc[10] = best0;
-    const u64 deadline = wall_clock64() + pa.persist_ticks;
-    sm.dl[0] = deadline;
-    sm.dl[1] = deadline + 10000000ull;  // +100 ms at 100 MHz: only a broken protocol gets here
-    sm.dl[2] = 0;
-  }
-  int bot = 0, top = 0;  // uniform
-  u64 popped = 0;        // uniform
-  int steps = 0, ndon = 0;
-  int nleaf = 0;
-  int best = best0;
-  bool full = false;
-  // [bot, top) -> [0, top - bot): blocks in ascending order, each read before written
-  auto compact = [&]() {
-    const int n = top - bot;
-    for (int base = 0; base < n; base += kBlock) {
-      const int i = base + tid;
-      uint4 x0, x1;
-      if (i < n) {
-        x0 = stk[2 * (bot + i)];
-        x1 = stk[2 * (bot + i) + 1];
-      }
-      __syncthreads();
-      if (i < n) st_node(stk + 2 * i, x0, x1, wt);
-      __syncthreads();
-    }
-    top = n;
-    bot = 0;
-  };
-  for (;;) {
-    int n = top - bot;
-    u64 g0 = 0;
-    int npop;
-    bool from_stack = n > 0;
-    if (!from_stack) {
-      bot = top = 0;
-      if (sl < nsl) {
-        g0 = sl * static_cast<u64>(grab);
-        npop = static_cast<int>(min(static_cast<u64>(grab), B - g0));
-        sl += static_cast<u64>(P);
-      } else {
-        // idle: wait for a donation, the end of the search, or the stop
-        vm_drain();
-        __syncthreads();
-        if (tid == 0) {
-          int got = 0;
-          const unsigned g = static_cast<unsigned>(sm.bc[9]) + 1;
-          const u64 hard = sm.dl[1];
-          const u64 t_wait = wall_clock64();
-          sm.bc[11] += 1;
-          if (!wt) {  // no dirty line of these slots may shadow a donation
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            vm_drain();
-          }
-          __hip_atomic_fetch_add(shard, (1ull << 32) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          vm_drain();  // counted idle before a donor can see the request
-          __hip_atomic_store(&box[me].want, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          for (unsigned spin = 0;; ++spin) {
-            const u64 m = __hip_atomic_load(&box[me].mail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (static_cast<unsigned>(persist_box_gen(m)) == g + 1) {
-              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-              vm_drain();
-              got = static_cast<int>(m & 0xffffffffu);
-              sm.bc[9] = static_cast<int>(g + 1);
-              break;
-            }
-            const u64 now = wall_clock64();
-            // workgroup 0 alone watches the shards; when every started workgroup is
-            // idle it tells each one through its box
-            bool end = false;
-            if (me == 0 && (spin & 3) == 3 && persist_all_idle(ws)) {
-              for (int j = 1; j < P; ++j)
-                __hip_atomic_store(&box[j].stop, v.pid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              end = true;
-            }
-            const bool stop = end || now > sm.dl[0] ||
-                              __hip_atomic_load(&box[me].stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v.pid;
-            if (stop || now > hard) {
-              unsigned e = g;
-              if (__hip_atomic_compare_exchange_strong(&box[me].want, &e, g + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT)) {
-                sm.bc[9] = static_cast<int>(g + 1);
-                if (now > hard) __hip_atomic_store(&pa.ctl->perr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-              // claimed: the donor's mail is on its way
-              if (now > hard + 10000000ull) {
-                __hip_atomic_store(&pa.ctl->perr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-            }
-            __builtin_amdgcn_s_sleep(4);
-          }
-          sm.dl[2] += wall_clock64() - t_wait;
-          sm.bc[6] = got;
-        }
-        __syncthreads();
-        const int got = __builtin_amdgcn_readfirstlane(sm.bc[6]);
-        __syncthreads();
-        if (got <= 0) break;
-        top = got;
-        n = got;
-        from_stack = true;
-      }
-    }
-    if (from_stack) {
-      // room for the children of a full pop (at most NJ - 1 per stack node)
-      if (top + kBlock * (NJ - 1) > lim && bot > 0) compact();
-      npop = min(min(n, kBlock), (lim - top) / (NJ - 1));
-      if (npop < 1) {
-        full = true;
-        break;
-      }
-    }
-    uint32_t w[8];
-    const bool valid = tid < npop;
-    if (valid) {
-      const uint4* src = from_stack
-                             ? stk + 2 * (top - npop + tid)
-                             : reinterpret_cast<const uint4*>(
-                                   pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool));
-      const uint4 x0 = src[0], x1 = src[1];
-      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
-      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
-    }
-    // in flight with the pops, parked in LDS (no register holds them across the
-    // bounds): the stop word and the incumbent (thread 0); with enough nodes to
-    // share, 16 random boxes (wave 0): the first waiting one is the candidate
-    // (staging slots bc[3], bc[10], bc[4], bc[7]: read by thread 0 only, after the scan's
-    // barriers, when every wave has read the previous step's broadcasts)
-    if (tid == 0) {
-      sm.bc[3] = __hip_atomic_load(&box[me].stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v.pid;
-      if ((steps & 15) == 15)  // the incumbent's line is shared: read now and then
-        sm.bc[10] = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const bool share = top - npop * from_stack - bot >= pa.persist_dmin;
-    if (share && tid < kWave) {
-      unsigned h = static_cast<unsigned>(me) * 0x9e3779b9u + static_cast<unsigned>(steps) * 0x85ebca6bu +
-                   static_cast<unsigned>(lane) * 0xc2b2ae35u;
-      h ^= h >> 15;
-      h *= 0x2c1b3c6du;
-      h ^= h >> 12;
-      const int r = static_cast<int>(h % static_cast<unsigned>(P));
-      unsigned wv = 0;
-      if (lane < 16 && r != me) wv = __hip_atomic_load(&box[r].want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const u64 odd = __ballot(wv & 1u);
-      const int first = odd ? __ffsll(static_cast<long long>(odd)) - 1 : -1;
-      if (lane == 0) sm.bc[4] = -1;
-      if (first >= 0 && lane == first) {
-        sm.bc[4] = r;
-        sm.bc[7] = static_cast<int>(wv);
-      }
-    }
-    if (from_stack) {
-      top -= npop;
-      popped += static_cast<u64>(npop);
-    }
-    ++steps;
-    uint32_t surv = 0;
-    int nsurv = 0;
-    if (valid) {
-      const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) {
-        if (leaf) {
-          ++nleaf;
-          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-        } else if (lb < best) {
-          ++nsurv;
-          surv |= 1u << k;
-        }
-      });
-    }
-    int tot = 0;
-    const int off = block_exclusive_scan(nsurv, sm.scan, &tot);
-    if (surv) emit_children<NJ>(w, surv, stk + 2 * (top + off), wt);
-    top += __builtin_amdgcn_readfirstlane(tot);
-    if (tid == 0) {
-      // every workgroup keeps its own deadline (nothing shared to poll)
-      const int stop = sm.bc[3] || wall_clock64() > sm.dl[0];
-      sm.bc[0] = stop;
-      sm.bc[2] = sm.bc[10];
-      sm.bc[5] = share ? sm.bc[4] : -1;
-      sm.bc[8] = sm.bc[7];
-    }
-    // pushes visible to the next step's pops (workgroup scope) + the broadcast
-    __syncthreads();
-    if (__builtin_amdgcn_readfirstlane(sm.bc[0])) break;
-    best = min(best, __builtin_amdgcn_readfirstlane(sm.bc[2]));
-    if (__builtin_amdgcn_readfirstlane(sm.bc[5]) >= 0 && top - bot >= pa.persist_dmin) {
-      __syncthreads();  // every wave has read bc[5]
-      if (tid == 0) {
-        const int r = sm.bc[5];
-        unsigned e = static_cast<unsigned>(sm.bc[8]);
-        int rr = -1;
-        if (__hip_atomic_compare_exchange_strong(&box[r].want, &e, e + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          // the receiver counts busy from now on (version + 1, idle - 1)
-          __hip_atomic_fetch_add(&ws->sh[r % kPersistShards].v, (1ull << 32) - 1ull, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-          rr = r;
-          sm.bc[8] = static_cast<int>(e + 1);
-        }
-        sm.bc[1] = rr;
-      }
-      __syncthreads();
-      const int r = __builtin_amdgcn_readfirstlane(sm.bc[1]);
-      if (r >= 0) {
-        const int h = (top - bot) / 2;
-        uint4* const dst = reinterpret_cast<uint4*>(bout + static_cast<size_t>(r) * cap);
-        for (int x = tid; x < h; x += kBlock) st_node(dst + 2 * x, stk[2 * (bot + x)], stk[2 * (bot + x) + 1], wt);
-        vm_drain();
-        __syncthreads();
-        if (tid == 0) {
-          if (!wt) {  // write-through payload: drained stores are already past every L2
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            vm_drain();
-          }
-          const u64 m = (static_cast<u64>(static_cast<unsigned>(sm.bc[8])) << 32) | static_cast<unsigned>(h);
-          __hip_atomic_store(&box[r].mail, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        bot += h;
-        ++ndon;
-      }
-    }
-  }
-  if (full && tid == 0) {  // the first to find a full stack tells every workgroup
-    int e = 0;
-    if (__hip_atomic_compare_exchange_strong(&ws->stop.v, &e, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT))
-      for (int j = 0; j < P; ++j) __hip_atomic_store(&box[j].stop, v.pid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // leave: the stack at the slot base, then this workgroup's untaken window slices on
-  // top (room was kept for them); they were counted when pushed, so they come off the
-  // tree count again (the next iteration counts its input chunks)
-  if (bot > 0) compact();
-  u64 back = 0;
-  for (; sl < nsl; sl += static_cast<u64>(P)) {
-    const u64 x = sl * static_cast<u64>(grab);
-    const int k = static_cast<int>(min(static_cast<u64>(grab), B - x));
-    if (tid < k) {
-      const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, x + tid, sm.pool));
-      const uint4 x0 = src[0], x1 = src[1];
-      stk[2 * (top + tid)] = x0;
-      stk[2 * (top + tid) + 1] = x1;
-    }
-    top += k;
-    back += static_cast<u64>(k);
-  }
-  for (int j = tid; j < R; j += kBlock) {
-    cnt_out[me * R + j] = max(0, min(G::SLOT, top - j * G::SLOT));
-    lcnt_out[me * R + j] = 0;
-  }
-  int leaves = 0;
-  (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
-  if (tid == 0) {
-    u64* rec = pa.pst + (static_cast<size_t>(t & 1) * P + me) * kPstWords;
-    rec[0] = popped - back;
-    rec[1] = static_cast<u64>(leaves);
-    rec[2] = static_cast<u64>(steps);
-    rec[3] = static_cast<u64>(ndon);
-    rec[4] = static_cast<u64>(sm.bc[11]);
-    rec[5] = sm.dl[2];
-  }
-}
-
-template <int NJ, int M, bool PK>
-__device__ inline void pfsp_expand_lb1_small(const PfspArgs<NJ, M>& a, int t) {
-  using G = PfspGeom<NJ, 1>;
-  using Node = PfspNode<NJ>;
-  constexpr int NWD = sizeof(Node) / 4;
-  static_assert(NJ <= 32 && sizeof(Node) == 32, "register path is for the 20-job bucket");
-  __shared__ PfspSmemLB1s<NJ, M> sm;
-  const int tid = threadIdx.x;
-  const auto& pa = a.pool;
-  // p table loads issued together with pool_begin's (one memory round trip)
-  constexpr int PTN = (NJ * PfspConsts<M>::MS + kBlock - 1) / kBlock;
-  uint16_t ptv[PTN];
-#pragma unroll
-  for (int i = 0; i < PTN; ++i) {
-    const int x = tid + i * kBlock;
-    ptv[i] = x < a.jobs * PfspConsts<M>::MS ? a.ptab[x] : 0;
-  }
-  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, PfspSmemLB1s<NJ, M>::BPF, G::LT, PK);
-  if (v.B == 0 || v.overflow) return;
-  {  // p table -> LDS (visible after the barrier below)
-    uint16_t* pt = &sm.ptab[0][0];
-#pragma unroll
-    for (int i = 0; i < PTN; ++i)
-      if (tid + i * kBlock < a.jobs * PfspConsts<M>::MS) pt[tid + i * kBlock] = ptv[i];
-  }
-  const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  Node* const bout = pa.buf[(t & 1) ^ 1];
-  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
-  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  pool_spill_leftovers<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, sm.pool);
-  __syncthreads();
-  if constexpr (PK) {
-    if (v.persist) {
-      lb1_small_persist<NJ, M>(a, sm, v, t, best);
-      return;
-    }
-  }
-  if (v.local) {
-    lb1_small_local<NJ, M>(a, sm, v, t, best);
-    return;
-  }
-  if (v.fused) {
-    lb1_small_two_level<NJ, M>(a, sm, v, t, best);
-    return;
-  }
-  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
-    const u64 gi = static_cast<u64>(ch) * G::BP + tid;
-    const bool valid = gi < v.B;
-    uint32_t w[NWD];
-    if (valid) {
-      const uint4* src = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool));
-      const uint4 x0 = src[0], x1 = src[1];
-      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
-      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
-    } else {
-#pragma unroll
-      for (int i = 0; i < NWD; ++i) w[i] = 0;
-    }
-    const int d = static_cast<int>(w[0] & 0xffu);
-    const bool leaf = d + 1 == a.jobs;
-    uint32_t surv = 0;
-    int nsurv = 0, nleaf = 0;
-    // child positions this rank keeps (all but in the split iteration); computed
-    // out of the unrolled loop so the hash costs no registers there
-    uint32_t kmask = ~0u;
-    if (v.split) {
-      kmask = 0;
-#pragma unroll 1
-      for (int k = 0; k < NJ; ++k) kmask |= split_keep(v, gi, k) ? (1u << k) : 0u;
-    }
-    int ninner = 0;
-    if (valid) {
-      lb1_small_parent<NJ, M, true>(
-          a, sm, w,
-          [&](int k, int lb) {
-            const bool keep = (kmask >> k) & 1u;
-            if (leaf) {
-              nleaf += keep;
-              if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-            } else if (keep && lb < best) {
-              ++nsurv;
-              surv |= 1u << k;
-            }
-          },
-          [&](int k, int lb, int lbl) {  // a child with one job left: explored here
-            if (((kmask >> k) & 1u) && lb < best) {
-              ++ninner;  // the child, pushed and expanded; its leaf counts as one more leaf
-              if (lbl < best) atomicMin(&pa.ctl->best.v, lbl);
-            }
-          });
-    }
-    // one scan for all counts, fields that cannot carry into each other: survivors
-    // (<= 256 x 19) in bits 0-12, leaf parents' leaves (<= 256) in 13-21, children
-    // explored in place (<= 512, one leaf each) in 22-31
-    int tot = 0;
-    const uint32_t packed = static_cast<uint32_t>(nsurv) | (static_cast<uint32_t>(nleaf) << 13) |
-                            (static_cast<uint32_t>(ninner) << 22);
-    const int off = block_exclusive_scan(static_cast<int>(packed), sm.scan, &tot) & 0x1fff;
-    if (tid == 0) {
-      const uint32_t u = static_cast<uint32_t>(tot);
-      const int inner = static_cast<int>(u >> 22);
-      cnt_out[ch] = static_cast<int>(u & 0x1fffu);
-      lcnt_out[ch] = (static_cast<int>((u >> 13) & 0x1ffu) + inner) | (inner << 16);
-    }
-    if (surv) {
-      const uint32_t jd = node_byte<NJ>(w, 1 + d);
-      uint32_t base[NWD];
-#pragma unroll
-      for (int i = 0; i < NWD; ++i) base[i] = w[i];
-      base[0] = (base[0] & ~0xffu) | static_cast<uint32_t>(d + 1);
-      uint4* dst = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off);
-      while (surv) {
-        const int k = __ffs(surv) - 1;
-        surv &= surv - 1;
-        uint32_t c[NWD];
-#pragma unroll
-        for (int i = 0; i < NWD; ++i) c[i] = base[i];
-        node_set<NJ>(c, 1 + d, node_byte<NJ>(w, 1 + k));
-        node_set<NJ>(c, 1 + k, jd);
-        dst[0] = make_uint4(c[0], c[1], c[2], c[3]);
-        dst[1] = make_uint4(c[4], c[5], c[6], c[7]);
-        dst += 2;
-      }
-    }
-  }
-}
-
 // LB1 / LB1_d expand: per chunk, thread p owns parent p end to end.
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
@@ -2148,23 +1346,7 @@ __global__ __launch_bounds__(kBlock) void pfsp_bounds_kernel(PfspArgs<NJ, M> a) 
   using G = PfspGeom<NJ, LBK, M>;
   using Node = PfspNode<NJ>;
   const int tid = threadIdx.x;
-  if constexpr (LBK != 2 && sizeof(Node) == 32) {
-    __shared__ PfspSmemLB1s<NJ, M> sm;
-    constexpr int MS = PfspConsts<M>::MS;
-    uint16_t* pt = &sm.ptab[0][0];
-    for (int i = tid; i < a.jobs * MS; i += kBlock) pt[i] = a.ptab[i];
-    __syncthreads();
-    for (int i = blockIdx.x * kBlock + tid; i < a.nparents; i += gridDim.x * kBlock) {
-      uint32_t w[8];
-      const uint4* src = reinterpret_cast<const uint4*>(a.parents_in + i);
-      const uint4 x0 = src[0], x1 = src[1];
-      w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
-      w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
-      const int d = static_cast<int>(w[0] & 0xffu);
-      int* out = a.bounds_out + a.offsets[i];
-      lb1_small_parent<NJ, M>(a, sm, w, [&](int k, int lb) { out[k - d] = lb; });
-    }
-  } else if constexpr (LBK != 2) {
+  if constexpr (LBK != 2) {
     constexpr int VPN = sizeof(Node) / 16;
     __shared__ PfspSmemLB1<NJ, M> sm;
     constexpr int MS = PfspConsts<M>::MS;

@@ -37,8 +37,6 @@ struct PoolCtl {
     int nch;    // chunks written by iteration t-1 into buffer t%2
     int sdone;  // armed rank split already done (see split_world)
     int qnext;  // chunk queue of kernels that deal chunks dynamically (LB2); reset by iteration t-1
-    int pers;   // iteration t-1 was persistent: its per-workgroup counts wait in pst[(t-1) & 1]
-    unsigned pid;  // iteration number (+1 per iteration): the epoch of a persistent iteration's stop words
   };
   Slot slot[3];
   // plain counters, updated by workgroup 0 (or the host between launches)
@@ -61,46 +59,13 @@ struct PoolCtl {
   int split_rank;
   int pad0;
   u64 split_min;
-  // persistent iterations: counts of the latest one when it ended a graph (finalize
-  // kernel; kPst* order: tree, sol, then the diagnostics), and the diagnostics so far
-  // (workgroup steps, donations, idle waits, wall-clock ticks spent waiting)
-  u64 pend_p[6];
-  u64 pdiag[4];
   // nodes pushed and leaves counted inside subtrees a thread explored to the end (N-Queens
   // finishing: 64-bit counts, one accumulator line per 8th of the grid; the host folds them)
   struct alignas(128) XAcc {
     u64 tree, sol;
     u64 pad[14];
   } xacc[8];
-  int perr;           // a persistent iteration's watchdog expired (nodes may be lost)
-  int pad1;
   CtlI32 best;      // incumbent (atomicMin by leaves)
-};
-
-// Work-sharing state of one persistent iteration (two, used by iterations of
-// alternating parity: iteration t works in ws[t & 1], its workgroup 0 clears
-// ws[(t + 1) & 1] for the next one). Workgroup g counts itself in shard g % 8 (each on
-// its own line: one hot word would serialise ~90 atomics/us): {version:32 |
-// started:16 | idle:16}, every update bumps the version. Termination: two collects of
-// the 8 shards that are identical (no update in between: a consistent snapshot) with
-// idle == started in each. A donor counts its receiver busy before it copies, so no
-// work is in flight in such a snapshot.
-constexpr int kPersistShards = 8;
-constexpr int kPstWords = 16;  // per-workgroup count record (one 128-B line): tree, sol, steps, donations, waits, wait ticks
-struct PersistWs {
-  CtlU64 sh[kPersistShards];
-  CtlI32 stop;  // a stack is full: the first to see it tells every workgroup (box stop words)
-};
-// One line per workgroup, polled by it alone (a line polled by every workgroup queues
-// each load behind the others: ~90 per us): its want generation (odd = waiting; a donor
-// claims it by CAS to even), the donor's {generation, count} mail, and the stop word
-// (== the iteration's pid: leave now; written by workgroup 0 when the search is over,
-// or by the workgroup that found a full stack).
-struct alignas(128) PersistBox {
-  unsigned want;
-  unsigned stop;
-  u64 mail;
-  u64 pad[14];
 };
 
 template <class Node>
@@ -117,25 +82,6 @@ struct PoolArgs {
   int fuse_max;     // two-level iterations for windows of at most this many parents (0: off)
   int local_steps;  // > 1: local DFS iterations of up to this many steps per chunk (kernels that have them)
   int local_min;    // wide local DFS when the pool holds at least this many parents (0: 4 grid windows)
-  int narrow_bp;    // narrow local DFS for windows of at most narrow_bp parents per workgroup (0: off)
-  int narrow_steps; // ... of up to this many steps per chunk
-  int narrow_cap;   // ... while the chunk's stack holds at most this many nodes
-  // Persistent iterations (kernels that implement them, see pool_begin): when the pool
-  // holds at least persist_min parents, persist_wg workgroups each run a depth-first
-  // search on a private stack (persist_r chunk slots) until the whole window's subtrees
-  // are explored or persist_ticks wall-clock ticks have passed, sharing work in the kernel:
-  // an idle workgroup posts an odd generation in box[wg].want; a donor claims it (CAS to
-  // even), copies the bottom half of its own stack into the receiver's slots and
-  // publishes {generation, count} in box[wg].mail (write-through payload, agent acquire).
-  u64 persist_min;  // 0: off
-  u64 persist_ticks;  // budget in wall-clock ticks (s_memrealtime)
-  int persist_wg;
-  int persist_r;
-  int persist_dmin; // smallest stack a donor splits
-  int persist_wt;   // stack writes write-through (sc1): no dirty stack line in any L2, no L2 write-back before a wait
-  PersistWs* pws;   // [2]
-  PersistBox* box;  // [persist_wg]
-  u64* pst;         // [2][persist_wg][kPstWords]: each workgroup's counts, folded by the next iteration / finalize
 };
 
 // Per-chunk leaf word: leaves in the low 16 bits; the high 16 bits count the
@@ -150,39 +96,6 @@ struct PoolSmem {
   int red[kBlock / kWave];
   u64 red64[kBlock / kWave][6];
 };
-
-// Sums of the persistent iteration's per-workgroup count records pst[parity] (one
-// workgroup; contains __syncthreads()).
-template <class Node, int MAXCHUNKS>
-__device__ inline void persist_sum(const PoolArgs<Node>& pa, int parity, PoolSmem<MAXCHUNKS>& ps, u64 (&s)[6]) {
-  u64 acc[6] = {0, 0, 0, 0, 0, 0};
-  const u64* rec = pa.pst + static_cast<size_t>(parity) * pa.persist_wg * kPstWords;
-  for (int i = threadIdx.x; i < pa.persist_wg; i += kBlock)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) acc[k] += rec[static_cast<size_t>(i) * kPstWords + k];
-#pragma unroll
-  for (int k = 0; k < 6; ++k)
-    for (int o = kWave / 2; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, kWave);
-  if ((threadIdx.x & (kWave - 1)) == 0)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) ps.red64[threadIdx.x / kWave][k] = acc[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    s[k] = 0;
-    for (int w = 0; w < kBlock / kWave; ++w) s[k] += ps.red64[w][k];
-  }
-  __syncthreads();
-}
-
-// Workgroup 0 of every iteration: clear the next iteration's work-sharing state.
-template <class Node>
-__device__ inline void persist_clear_next(const PoolArgs<Node>& pa, int t) {
-  if (!pa.pws) return;
-  PersistWs* n = pa.pws + ((t + 1) & 1);
-  if (threadIdx.x < kPersistShards) n->sh[threadIdx.x].v = 0;
-  if (threadIdx.x == kPersistShards) n->stop.v = 0;
-}
 
 // Exclusive prefix of cnt[0..n) into pre[0..n] (pre[n] = total) by one workgroup.
 template <int MAXCHUNKS>
@@ -227,9 +140,7 @@ struct IterView {
   int steps;          // local DFS: steps per chunk at most
   int cap;            // local DFS: no further step once the stack holds more than this
   int srank, sworld;
-  bool persist;       // persistent iteration: work-sharing depth-first search in one kernel
   bool armed;         // a rank split is pending: the pool is replicated on every rank
-  unsigned pid;       // iteration number (Slot::pid)
 };
 
 // Does this rank keep child position k of window parent gi? (always, outside the
@@ -259,13 +170,8 @@ template <class Node, int MAXCHUNKS>
 // of its chunk's own slot region — a private stack in L2 — for up to local_steps
 // levels; what is left on the stack is the chunk's output. Several tree levels per
 // dependent kernel, and the next iteration re-deals the stacks over the grid.
-//
-// Persistent iterations (PER, kernels that implement them; pa.persist_min > 0): a
-// window of at least persist_min parents, outside a pending rank split, is explored
-// to the end inside one kernel (or for pa.persist_ticks): persist_wg x persist_r
-// chunks are written (each workgroup's stack left over), no other mode applies.
 __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, PoolSmem<MAXCHUNKS>& ps,
-                                      int BPF = 0, int LT = 1, bool PER = false) {
+                                      int BPF = 0, int LT = 1) {
   const int s_in = t % 3, s_out = (t + 1) % 3;
   const int b_in = t & 1;
   PoolCtl* ctl = pa.ctl;
@@ -275,7 +181,6 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // ms, profiles/r1/r1q: cold count lines), though ta008 gained 4 %.
   IterView v;
   v.S = ctl->slot[s_in].stack;
-  v.pid = ctl->slot[s_in].pid;
   v.nch_in = ctl->slot[s_in].nch;
   const int done_in = ctl->slot[s_in].sdone;
   v.bot = ctl->bot;
@@ -287,7 +192,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     // and leave — no table staging, no scans, no counter traffic
     v.C = v.B = v.nb = v.ns = v.L = v.Snew = v.bot = 0;
     v.nchunks = 0;
-    v.overflow = v.split = v.fused = v.local = v.persist = v.armed = false;
+    v.overflow = v.split = v.fused = v.local = v.armed = false;
     v.bp = BP;
     v.steps = v.cap = 0;
     v.srank = v.sworld = 0;
@@ -295,10 +200,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
       ctl->slot[s_out].stack = 0;
       ctl->slot[s_out].nch = 0;
       ctl->slot[s_out].sdone = done_in;
-      ctl->slot[s_out].pers = 0;
-      ctl->slot[s_out].pid = v.pid + 1;
     }
-    if (PER && blockIdx.x == 0) persist_clear_next(pa, t);
     return v;
   }
   // uniform by construction: readfirstlane keeps the window arithmetic in SGPRs
@@ -311,23 +213,13 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // (the split must see every level). Below that, breadth (one level per kernel,
   // every chunk short) keeps the grid busier than chunks that step for different
   // lengths. A local window is one chunk per workgroup, at most BP parents each: a
-  // workgroup's steps are not queued behind another chunk's.
-  //
-  // Narrow local DFS for windows of at most pa.narrow_bp parents per workgroup (the
-  // ramp-up, the tail, a rank's share after a split): every workgroup follows its
-  // few subtrees for up to pa.narrow_steps levels — a level costs one LDS/L2 step
-  // instead of one dependent kernel — and hands its stack back to the grid as soon
-  // as it holds more than pa.narrow_cap nodes (the subtree turned wide).
+  // workgroup's steps are not queued behind another chunk's. (A narrow-window variant
+  // for the ramp-up and the tail measured slower and was removed: profiles/r2/.)
   const u64 full = static_cast<u64>(gridDim.x) * BP;
   const u64 lmin = pa.local_min > 0 ? static_cast<u64>(pa.local_min) : 4 * full;
-  const bool per = PER && pa.persist_min > 0 && !armed && v.S + v.C >= pa.persist_min;
-  v.persist = per;
-  const bool wide = !per && LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= max(lmin, full);
-  const bool narrow = !per && !wide && LT > 1 && pa.narrow_steps > 1 && !armed &&
-                      v.B <= static_cast<u64>(gridDim.x) * static_cast<u64>(pa.narrow_bp);
-  v.local = wide || narrow;
-  v.steps = wide ? pa.local_steps : pa.narrow_steps;
-  v.cap = wide ? 0x7fffffff : pa.narrow_cap;
+  v.local = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= max(lmin, full);
+  v.steps = pa.local_steps;
+  v.cap = 0x7fffffff;
   if (v.local) v.B = min(v.B, full);
   v.nb = min(v.B, v.C);
   v.ns = v.B - v.nb;
@@ -337,7 +229,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // a pending split needs the whole (replicated) pool inside the window
   const bool bad_split = armed && v.B < v.S + v.C;
   v.split = armed && !bad_split && v.B >= split_min;
-  v.fused = !per && !v.local && BPF > 0 && !armed && v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
+  v.fused = !v.local && BPF > 0 && !armed && v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
   int bp = v.fused ? BPF : BP;
   if (v.local) {
     // spread a window smaller than the grid over every workgroup
@@ -345,7 +237,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     bp = static_cast<int>(min(static_cast<u64>(BP), max(per, 1ull)));
   }
   v.bp = bp;
-  v.nchunks = per ? pa.persist_wg * pa.persist_r : static_cast<int>((v.B + bp - 1) / bp);
+  v.nchunks = static_cast<int>((v.B + bp - 1) / bp);
   const bool overflow = v.overflow;
   v.overflow = overflow || bad_split;
   if (blockIdx.x == 0) {
@@ -359,23 +251,10 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     int lf_total = 0, in_total = 0;
     (void)block_exclusive_scan(lf, ps.red, &lf_total);
     (void)block_exclusive_scan(in, ps.scan, &in_total);
-    // counts of a persistent previous iteration (explored tree, leaves, diagnostics)
-    // (kernels with persistent iterations only: in an engine that has them every
-    // iteration runs such a kernel, and the host folds them before anything else runs)
-    u64 pc[6] = {0, 0, 0, 0, 0, 0};
-    if (PER && ctl->slot[s_in].pers) persist_sum<Node, MAXCHUNKS>(pa, (t + 1) & 1, ps, pc);
     if (threadIdx.x == 0) {
       ctl->slot[s_out].stack = v.overflow ? v.S : v.Snew;
       ctl->slot[s_out].nch = v.overflow ? 0 : v.nchunks;
       ctl->slot[s_out].sdone = (done_in || v.split) ? 1 : 0;
-      ctl->slot[s_out].pers = (!v.overflow && v.persist) ? 1 : 0;
-      ctl->slot[s_out].pid = v.pid + 1;
-      if (PER) {
-        ctl->tree += pc[0];
-        ctl->sol += pc[1];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ctl->pdiag[k] += pc[2 + k];
-      }
       if (v.split && v.srank != 0) {
         // everything counted so far was explored identically by every rank: rank 0 keeps it
         ctl->tree = 0;
@@ -391,8 +270,6 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
       if (overflow) ctl->overflow = 1;
       else if (bad_split) ctl->overflow = 2;
     }
-    // the next iteration's work-sharing state (nobody uses it during this one)
-    if (PER) persist_clear_next(pa, t);
   }
   return v;
 }
@@ -487,8 +364,7 @@ __global__ __launch_bounds__(kBlock) void pool_weight_kernel(const Node* __restr
 // the sequence number last (release): the host polls that word instead of
 // waiting for the graph's completion signal (engine.hpp wait_oldest).
 // (b: the buffer the graph's last iteration wrote — graphs of 3k iterations end at phase 0
-// or 3: slot 0 either way, buffer b = phase & 1; that iteration's persistent records are
-// pst[b ^ 1])
+// or 3: slot 0 either way, buffer b = phase & 1)
 template <class Node, int MAXCHUNKS>
 __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa, int b) {
   __shared__ PoolSmem<MAXCHUNKS> ps;
@@ -505,15 +381,10 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   (void)block_exclusive_scan(c, ps.scan, &ct);
   (void)block_exclusive_scan(l, ps.red, &lt);
   (void)block_exclusive_scan(in, ps.scan, &it);
-  // the graph's last iteration was persistent: its counts
-  u64 pc[6] = {0, 0, 0, 0, 0, 0};
-  if (pa.ctl->slot[0].pers) persist_sum<Node, MAXCHUNKS>(pa, b ^ 1, ps, pc);
   if (threadIdx.x == 0) {
     pa.ctl->pend_children = static_cast<u64>(ct);
     pa.ctl->pend_leaves = static_cast<u64>(lt);
     pa.ctl->pend_internal = static_cast<u64>(it);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) pa.ctl->pend_p[k] = pc[k];
     pa.ctl->seq = seq;
   }
   // publish the whole control block to host-mapped memory: the host reads it
@@ -523,7 +394,6 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   constexpr int kPl = static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4);
   constexpr int kPi = static_cast<int>(offsetof(PoolCtl, pend_internal) / 4);
   constexpr int kSeq = static_cast<int>(offsetof(PoolCtl, seq) / 4);
-  constexpr int kPp = static_cast<int>(offsetof(PoolCtl, pend_p) / 4);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pa.ctl);
   uint32_t* dst = reinterpret_cast<uint32_t*>(pa.mirror);
   for (int i = threadIdx.x; i < static_cast<int>(sizeof(PoolCtl) / 4); i += kBlock) {
@@ -535,7 +405,6 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
     if (i == kPl + 1) x = 0;
     if (i == kPi) x = static_cast<uint32_t>(it);
     if (i == kPi + 1) x = 0;
-    if (i >= kPp && i < kPp + 12) x = static_cast<uint32_t>(pc[(i - kPp) >> 1] >> (((i - kPp) & 1) * 32));
     __hip_atomic_store(dst + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();

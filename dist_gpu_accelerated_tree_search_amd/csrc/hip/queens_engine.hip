@@ -15,7 +15,6 @@ struct QueensTraits {
   static constexpr int kChildrenPerChunk = S::MAXCH;
   static constexpr int kMaxChildren = S::MAXCH / S::BP;
   static constexpr int kLocalSteps = 1;
-  static constexpr bool kPersist = false;
   static constexpr int kMaxChunks = S::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL(dev::queens_expand_kernel, dim3(grid), dim3(dev::kBlock), 0, s, a, t);
@@ -33,8 +32,6 @@ struct QueensTraits {
       return 1;
     return n;
   }
-  static void launch_persist(const Args&, int, int, hipStream_t) {}
-  static int blocks_per_cu_persist() { return 0; }
 };
 
 static dev::QueensArgs queens_args(int N, int G) {

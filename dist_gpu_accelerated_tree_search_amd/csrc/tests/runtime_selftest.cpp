@@ -88,6 +88,8 @@ int main() {
   }
   runner_case(PfspProblem<20>(in, 0), 3, 1, seq_ub.tree, seq_ub.sol, seq.best, seq.best, 30);
   runner_case(PfspProblem<20>(in, 0), 2, 3, seq_ub.tree, seq_ub.sol, seq.best, seq.best, 0);
+  // front-carrying nodes (the layout the engines use for LB1 / LB1_d on 20 jobs)
+  runner_case(PfspFrontProblem<5>(in, 0), 3, 2, seq_ub.tree, seq_ub.sol, seq.best, seq.best, 30);
   runner_case(QueensProblem(10, 1), 4, 2, 35538ull, 724ull, 0, 0, 50);
   std::printf(failures ? "SELFTEST FAILED\n" : "SELFTEST OK\n");
   return failures ? 1 : 0;

@@ -66,7 +66,11 @@ class PfspModel:
         self.jobs = self.native.jobs
         self.machines = self.native.machines
         self.best_known = self.native.best_known
-        self.node_bytes = nodes_mod.pfsp_node_bytes(self.jobs)
+        # engines' node layout: front nodes (depth, unscheduled set, per-machine
+        # completion times; csrc/core/pfsp_front.hpp) for LB1 / LB1_d on instances of
+        # up to 20 jobs, the permutation node of the job-count bucket otherwise
+        self.front_layout = bool(C.pfsp_front_layout(self.native, lb))
+        self.node_bytes = int(C.pfsp_engine_node_bytes(self.native, lb))
 
     @classmethod
     def synthetic(cls, jobs: int, machines: int, seed: int, lb: int = 1) -> "PfspModel":
@@ -79,7 +83,12 @@ class PfspModel:
 
     # ---- host steps ----
     def root(self) -> np.ndarray:
-        return nodes_mod.pfsp_root(self.jobs)
+        """Root node in the engines' layout, shape (1, node_bytes)."""
+        return ops.cpu().pfsp_root(self.native, self.lb)
+
+    def to_engine_layout(self, perm_nodes: np.ndarray) -> np.ndarray:
+        """Permutation-layout nodes (utils.nodes.pfsp_pack) in the engines' layout."""
+        return ops.cpu().pfsp_to_engine_layout(self.native, self.lb, np.ascontiguousarray(perm_nodes, dtype=np.uint8))
 
     @property
     def host_lb(self) -> int:

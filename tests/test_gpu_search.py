@@ -256,22 +256,3 @@ def test_learned_first_replay_then_longer_tree():
     assert (r.tree, r.sol, r.best) == GOLDEN[(14, 1)]
 
 
-@pytest.mark.parametrize("key", [(14, 1), (14, 0), (7, 0), (13, 1), (3, 1), (12, 0)])
-def test_last_level_finishing_goldens(key, monkeypatch):
-    # TTS_LB1_FIN=1: parents with two jobs left evaluate their children's complete
-    # schedules in place; the counts must not change
-    monkeypatch.setenv("TTS_LB1_FIN", "1")
-    m = PfspModel(*key)
-    eng = m.make_engine("gpu", 0, SMALL)
-    for _ in range(2):
-        r = solve_engine(m, eng)
-        assert (r.tree, r.sol, r.best) == GOLDEN[key]
-
-
-def test_last_level_finishing_with_split(monkeypatch):
-    monkeypatch.setenv("TTS_LB1_FIN", "1")
-    model = PfspModel(14, 1)
-    opts = EngineOptions(ring_bytes=1 << 29, max_parents=1 << 16)
-    nodes, tree1, sol1, best = model.warmup(model.initial_best(1), 25)
-    tree, sol, per, done = _split_solve(model, 4, 2048, opts, nodes, best)
-    assert (tree + tree1, sol + sol1) == GOLDEN[(14, 1)][:2] and all(done)

@@ -32,9 +32,11 @@ def test_bfs_nodes_are_valid_children():
     inst = C.PfspInstance.taillard(14)
     nodes, tree, sol, best = C.pfsp_bfs(inst, 0, 1377, 100)
     assert len(nodes) >= 100 and tree > 0 and best == 1377
-    d, p = nd.pfsp_unpack(nodes, 20)
-    for row in p:
-        assert sorted(row.tolist()) == list(range(20))
+    # LB1_d on 20 jobs: front nodes (depth, unscheduled set, fronts)
+    d, rest, fr = nd.pfsp_front_unpack(nodes, 10)
+    for depth, r in zip(d, rest):
+        assert bin(int(r)).count("1") == 20 - depth
+    assert (fr[:, 1:] >= fr[:, :-1]).all()  # completion times grow along the machines
     # draining the warm-up frontier completes the golden tree
     t2, s2, b2 = C.pfsp_drain(inst, 0, 1377, nodes)
     assert (tree + t2, sol + s2, b2) == (2573652, 2648, 1377)
