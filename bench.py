@@ -49,12 +49,20 @@ def log(*a):
 
 
 class Emitter:
-    """Prints the single JSON line exactly once (main thread or watchdog)."""
+    """Prints the single JSON line exactly once (main thread or watchdog).
 
-    def __init__(self, rank: int):
-        self.rank = rank
+    Everything else a process writes to its standard output — including native
+    libraries writing to file descriptor 1 directly (gloo's connection banner, HIP or
+    RCCL messages) — goes to stderr: fd 1 is pointed at stderr for the whole run and
+    the line is written through a private duplicate of the original stdout."""
+
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", "0"))
         self.lock = threading.Lock()
         self.done = False
+        sys.stdout.flush()
+        self.fd = os.dup(1)
+        os.dup2(2, 1)
 
     def emit(self, rec: dict) -> None:
         with self.lock:
@@ -62,7 +70,7 @@ class Emitter:
                 return
             self.done = True
             if self.rank == 0:
-                print(json.dumps(rec), flush=True)
+                os.write(self.fd, (json.dumps(rec) + "\n").encode())
 
 
 def main() -> int:
@@ -90,6 +98,7 @@ def main() -> int:
     ap.add_argument("--extra-inst-lb2", type=int, default=56, help=argparse.SUPPRESS)
     ap.add_argument("--extra-ring-gb", type=float, default=64.0)
     a = ap.parse_args()
+    out = Emitter()  # before anything can write to stdout
 
     import torch  # noqa: F401  (before the HIP extension: one HIP runtime per process)
 
@@ -103,7 +112,6 @@ def main() -> int:
     comm = Comm(use_gpu=(a.backend == "gpu" and a.comm == "nccl"), device=a.device)
     if comm.preflight is not None:
         log(f"rank {comm.rank}: RCCL point-to-point preflight ok: {comm.preflight}")
-    out = Emitter(comm.rank)
     model = PfspModel(a.inst, a.lb)
     opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * (1 << 30)))
     device = (comm.topo.local_rank if a.device is None else a.device) if a.backend == "gpu" else 0

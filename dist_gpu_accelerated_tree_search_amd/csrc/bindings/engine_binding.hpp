@@ -16,6 +16,7 @@
 #include "../core/dist_rounds.hpp"
 #include "../core/dist_session.hpp"
 #include "../core/engine_api.hpp"
+#include "../core/hybrid_engine.hpp"
 #include "../core/runner.hpp"
 #include "../core/shm_control.hpp"
 
@@ -43,6 +44,8 @@ inline py::dict engine_stats_dict(const EngineStats& s) {
   d["exports"] = s.exports;
   d["imports"] = s.imports;
   d["pinned_bytes"] = s.pinned_bytes;
+  d["cpu_tree"] = s.cpu_tree;
+  d["cpu_sol"] = s.cpu_sol;
   return d;
 }
 
@@ -119,6 +122,18 @@ inline void bind_engine(py::module_& m) {
            "Wait on the host for every copy enqueued so far.")
       .def("pool_weight", &IEngine::pool_weight, py::arg("w"), py::call_guard<py::gil_scoped_release>(),
            "Sum over the pool of w[depth] (progress measure, see search.progress_weights).");
+  m.def(
+      "make_hybrid_engine",
+      [](py::object gpu, py::object cpu, size_t m_, size_t cpu_cap) -> std::unique_ptr<IEngine> {
+        HybridConfig c;
+        c.m = std::max<size_t>(1, m_);
+        c.cpu_cap = std::max<size_t>(1, cpu_cap);
+        return std::make_unique<HybridEngine>(gpu.cast<IEngine*>(), cpu.cast<IEngine*>(), c);
+      },
+      py::arg("gpu"), py::arg("cpu"), py::arg("m") = 25, py::arg("cpu_cap") = 20000, py::keep_alive<0, 1>(),
+      py::keep_alive<0, 2>(),
+      "One rank's engine: `gpu` on the calling thread plus the CPU worker `cpu` on its own thread, sharing work "
+      "and the incumbent (core/hybrid_engine.hpp; ref -C 1 in the distributed driver).");
 }
 
 // Intra-node control plane (csrc/core/shm_control.hpp), bound in both modules so the
@@ -235,15 +250,17 @@ inline RoundHook hook_from(py::object round_hook) {
 // per-rank table as two arrays (one row per rank): cheap to hand to Python
 inline py::dict outcome_dict(const DistOutcome& out) {
   const py::ssize_t W = static_cast<py::ssize_t>(out.tree.size());
-  py::array_t<int64_t> iv({W, static_cast<py::ssize_t>(11)});
+  py::array_t<int64_t> iv({W, static_cast<py::ssize_t>(13)});
   py::array_t<double> fv({W, static_cast<py::ssize_t>(7)});
   auto I = iv.mutable_unchecked<2>();
   auto F = fv.mutable_unchecked<2>();
   for (py::ssize_t r = 0; r < W; ++r) {
-    const unsigned long long cols[11] = {out.tree[r], out.sol[r], out.sent[r], out.received[r], out.transfers_in[r],
+    auto at = [&](const std::vector<unsigned long long>& v) { return r < static_cast<py::ssize_t>(v.size()) ? v[r] : 0ull; };
+    const unsigned long long cols[13] = {out.tree[r], out.sol[r], out.sent[r], out.received[r], out.transfers_in[r],
                                          out.transfers_out[r], out.steals[r], out.success_steals[r],
-                                         out.idle_rounds[r], out.early_rounds[r], out.dropped[r]};
-    for (int k = 0; k < 11; ++k) I(r, k) = static_cast<int64_t>(cols[k]);
+                                         out.idle_rounds[r], out.early_rounds[r], out.dropped[r], at(out.cpu_tree),
+                                         at(out.cpu_sol)};
+    for (int k = 0; k < 13; ++k) I(r, k) = static_cast<int64_t>(cols[k]);
     const double dc[7] = {out.t_run[r], out.t_comm[r], out.t_idle[r], out.t_termination[r], out.t_load_bal[r],
                           out.t_memcpy[r], out.t_malloc[r]};
     for (int k = 0; k < 7; ++k) F(r, k) = dc[k];
@@ -253,7 +270,8 @@ inline py::dict outcome_dict(const DistOutcome& out) {
   d["complete"] = out.complete;
   d["rounds"] = out.rounds;
   d["watchdog_events"] = out.watchdog_events;
-  d["counts"] = iv;  // tree sol sent received transfers_in transfers_out steals success_steals idle_rounds early_rounds dropped
+  d["counts"] = iv;  // tree sol sent received transfers_in transfers_out steals success_steals idle_rounds
+                     // early_rounds dropped cpu_tree cpu_sol (CPU-worker share of a hybrid rank)
   d["times"] = fv;   // t_run t_comm t_idle t_termination t_load_bal t_memcpy t_malloc
   return d;
 }

@@ -177,7 +177,7 @@ struct DistOutcome {
   bool complete = true;
   unsigned long long rounds = 0;
   std::vector<unsigned long long> tree, sol, sent, received, transfers_in, transfers_out, steals, success_steals,
-      idle_rounds, early_rounds, dropped;
+      idle_rounds, early_rounds, dropped, cpu_tree, cpu_sol;
   std::vector<double> t_run, t_comm, t_idle, t_termination, t_load_bal, t_memcpy, t_malloc;
   unsigned long long watchdog_events = 0;
 };
@@ -392,13 +392,15 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
 
   // ---- final reductions: two all-gathers (counters, times) ----
   const EngineStats es = e.stats();
-  const int64_t iv[13] = {static_cast<int64_t>(es.tree), static_cast<int64_t>(es.sol), static_cast<int64_t>(sent),
-                          static_cast<int64_t>(received), static_cast<int64_t>(tin), static_cast<int64_t>(tout),
-                          static_cast<int64_t>(steals), static_cast<int64_t>(ssteals), static_cast<int64_t>(idle_rounds),
-                          static_cast<int64_t>(early), static_cast<int64_t>(dropped), es.best,
-                          static_cast<int64_t>(wd_events.load())};
-  std::vector<int64_t> ia(static_cast<size_t>(world) * 13);
-  ctl.allgather(iv, 13, ia.data(), [] {});
+  constexpr int kIv = 15;
+  const int64_t iv[kIv] = {static_cast<int64_t>(es.tree), static_cast<int64_t>(es.sol), static_cast<int64_t>(sent),
+                           static_cast<int64_t>(received), static_cast<int64_t>(tin), static_cast<int64_t>(tout),
+                           static_cast<int64_t>(steals), static_cast<int64_t>(ssteals),
+                           static_cast<int64_t>(idle_rounds), static_cast<int64_t>(early),
+                           static_cast<int64_t>(dropped), es.best, static_cast<int64_t>(wd_events.load()),
+                           static_cast<int64_t>(es.cpu_tree), static_cast<int64_t>(es.cpu_sol)};
+  std::vector<int64_t> ia(static_cast<size_t>(world) * kIv);
+  ctl.allgather(iv, kIv, ia.data(), [] {});
   double dv[7] = {t_run, t_comm, t_idle, t_term, t_lb, es.t_memcpy, es.t_malloc};
   int64_t dvi[7];
   std::memcpy(dvi, dv, sizeof(dv));
@@ -408,7 +410,7 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
   out.best = 0x7fffffff;
   auto col = [&](int k) {
     std::vector<unsigned long long> v(world);
-    for (int r = 0; r < world; ++r) v[r] = static_cast<unsigned long long>(ia[r * 13 + k]);
+    for (int r = 0; r < world; ++r) v[r] = static_cast<unsigned long long>(ia[r * kIv + k]);
     return v;
   };
   out.tree = col(0);
@@ -422,9 +424,11 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
   out.idle_rounds = col(8);
   out.early_rounds = col(9);
   out.dropped = col(10);
+  out.cpu_tree = col(13);
+  out.cpu_sol = col(14);
   for (int r = 0; r < world; ++r) {
-    out.best = std::min<int>(out.best, static_cast<int>(ia[r * 13 + 11]));
-    out.watchdog_events += static_cast<unsigned long long>(ia[r * 13 + 12]);
+    out.best = std::min<int>(out.best, static_cast<int>(ia[r * kIv + 11]));
+    out.watchdog_events += static_cast<unsigned long long>(ia[r * kIv + 12]);
   }
   auto dcol = [&](int k) {
     std::vector<double> v(world);

@@ -110,6 +110,8 @@ inline DistSolveResult dist_solve_split(IEngine& e, RoundControl& ctl, const Dis
     for (auto* v : {&o1.sent, &o1.received, &o1.transfers_in, &o1.transfers_out, &o1.steals, &o1.success_steals,
                     &o1.idle_rounds, &o1.early_rounds, &o1.dropped})
       one(*v, 0ull);
+    one(o1.cpu_tree, st.cpu_tree);
+    one(o1.cpu_sol, st.cpu_sol);
     one(o1.t_run, st.t_run);
     one(o1.t_memcpy, st.t_memcpy);
     one(o1.t_malloc, st.t_malloc);

@@ -39,6 +39,9 @@ struct EngineStats {
   size_t pinned_bytes = 0;  // pinned host spill blocks held
   double t_run = 0, t_memcpy = 0, t_malloc = 0;
   size_t device_nodes = 0, host_nodes = 0, capacity = 0;
+  // share of tree / sol explored by the CPU worker of a hybrid rank engine
+  // (core/hybrid_engine.hpp); 0 for plain engines
+  unsigned long long cpu_tree = 0, cpu_sol = 0;
 };
 
 // Type-erased interface used by the Python bindings and the native CLIs.

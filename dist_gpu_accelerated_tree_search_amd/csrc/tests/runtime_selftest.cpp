@@ -11,6 +11,7 @@
 
 #include "../core/cpu_engine.hpp"
 #include "../core/drivers_cpu.hpp"
+#include "../core/hybrid_engine.hpp"
 #include "../core/runner.hpp"
 
 using namespace tts;
@@ -91,6 +92,25 @@ int main() {
   // front-carrying nodes (the layout the engines use for LB1 / LB1_d on 20 jobs)
   runner_case(PfspFrontProblem<5>(in, 0), 3, 2, seq_ub.tree, seq_ub.sol, seq.best, seq.best, 30);
   runner_case(QueensProblem(10, 1), 4, 2, 35538ull, 724ull, 0, 0, 50);
+  {  // hybrid rank engine (main engine + CPU worker thread), small batches: many hand-overs
+    CpuEngine<PfspFrontProblem<5>> main_eng(PfspFrontProblem<5>(in, 0), 16, 1), cpu_eng(PfspFrontProblem<5>(in, 0), 16, 2);
+    HybridConfig hc;
+    hc.m = 4;
+    hc.cpu_cap = 64;
+    HybridEngine h(&main_eng, &cpu_eng, hc);
+    const auto root = PfspFrontProblem<5>(in, 0).root();
+    for (int rep = 0; rep < 2; ++rep) {
+      const EngineStats st = h.solve_from(&root, 1, seq.best);
+      std::printf("hybrid: tree %llu sol %llu (cpu worker %llu) best %d\n", st.tree, st.sol, st.cpu_tree, st.best);
+      CHECK(st.tree == seq_ub.tree && st.sol == seq_ub.sol && st.best == seq.best);
+      CHECK(st.cpu_tree > 0);
+    }
+    // time-sliced like the round loop
+    h.begin(&root, 1, seq.best);
+    while (h.size() > 0) h.run(-1, 0.002, 1);
+    const EngineStats st = h.stats();
+    CHECK(st.tree == seq_ub.tree && st.sol == seq_ub.sol);
+  }
   std::printf(failures ? "SELFTEST FAILED\n" : "SELFTEST OK\n");
   return failures ? 1 : 0;
 }

@@ -53,6 +53,13 @@ class QueensModel:
                                     iters_large=opts.iters_large, use_graphs=opts.use_graphs,
                                     iters_first=opts.iters_first)
 
+    def make_hybrid(self, engine, backend: str, threads: int, m: int = 25, cap: int = 20000, batch: int = 5000):
+        """`engine` plus a CPU worker of `threads` threads as one rank engine
+        (csrc/core/hybrid_engine.hpp)."""
+        mod = ops.hip() if backend == "gpu" else ops.cpu()
+        cpu = mod.make_queens_cpu_engine(self.N, self.G, batch, threads)
+        return mod.make_hybrid_engine(engine, cpu, m, cap)
+
     def labels_cpu(self, nodes: np.ndarray) -> np.ndarray:
         """labels[i, r] = 1 iff row r is free and diagonal-safe for parent i."""
         cols, diag, anti, depth = nodes_mod.queens_unpack(nodes)

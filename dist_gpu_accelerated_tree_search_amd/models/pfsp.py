@@ -121,6 +121,18 @@ class PfspModel:
                                   use_graphs=opts.use_graphs, taillard_id=self.inst_id,
                                   iters_first=opts.iters_first)
 
+    def make_hybrid(self, engine, backend: str, threads: int, m: int = 25, cap: int = 20000, batch: int = 5000):
+        """`engine` plus a CPU worker of `threads` threads as one rank engine
+        (csrc/core/hybrid_engine.hpp; ref -C 1 of the distributed driver). The CPU
+        worker evaluates LB1 as LB1_d (same values, ref pfsp_multigpu_cuda.c:152-154)."""
+        if backend == "gpu":
+            H = ops.hip()
+            cpu = H.make_pfsp_cpu_engine(self.jobs, self.machines, list(self.native.p), self.lb, batch, threads)
+            return H.make_hybrid_engine(engine, cpu, m, cap)
+        C = ops.cpu()
+        cpu = C.make_pfsp_cpu_engine(self.native, self.host_lb, batch, threads)
+        return C.make_hybrid_engine(engine, cpu, m, cap)
+
     # ---- bounds (reference evaluate_gpu semantics; used by tests/tools) ----
     def child_bounds_cpu(self, nodes: np.ndarray, best: int = INT_MAX) -> np.ndarray:
         C = ops.cpu()

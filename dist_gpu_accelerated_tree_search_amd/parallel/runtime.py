@@ -85,6 +85,12 @@ class DistConfig:
     # exchange the incumbent through the node-wide board after every graph replay
     # (ref checkBest around every batch); False: only at round boundaries
     live_best: bool = True
+    # CPU worker next to each rank's GPU (ref -C 1 in pfsp_dist_multigpu_cuda.c:161-162,
+    # 471-575): threads of the rank's CPU engine (0: none) and its batch (ref -T; a CPU
+    # thief takes at most 4*T nodes). parallel/workers.py wraps the engines into one
+    # hybrid engine (csrc/core/hybrid_engine.hpp)
+    cpu_workers: int = 0
+    cpu_batch: int = 5000
     # failure detection / fault injection (parallel/faults.py; env TTS_FAULT_*)
     watchdog_s: float = 0.0
     watchdog_abort: bool = False
@@ -249,7 +255,7 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, t_start: float, t_init: 
     gbest = min(int(out["best"]), int(best))
     elapsed = time.perf_counter() - t_start
     return SolveResult(best=gbest, tree=tree, sol=sol, elapsed=elapsed, t_init=t_init,
-                       t_search=t_search, t_tail=0.0, workers=RankTable(cnt, tms),
+                       t_search=t_search, t_tail=0.0, workers=RankTable(cnt, tms, bool(cfg.cpu_workers)),
                        extra={"rounds": int(out["rounds"]), "sent_nodes": cnt[:, 2].tolist(),
                               "received_nodes": cnt[:, 3].tolist(), "world": world,
                               "complete": bool(out["complete"]), "dropped_transfers": int(cnt[:, 10].sum()),
@@ -258,26 +264,32 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, t_start: float, t_init: 
 
 
 class RankTable(list):
-    """Per-rank WorkerStats, built from the native round loop's count/time arrays on
+    """Per-worker WorkerStats, built from the native round loop's count/time arrays on
     first use (the bench never needs them inside its timed loop). Fields keep the
     reference's meaning (ref PFSP_statistic.c:82-84, 133-135): gen_child = children the
     rank pushed (indexChildren), steals = rounds it asked for work, success_steals =
-    rounds it received some, terminations = rounds it stayed idle."""
+    rounds it received some, terminations = rounds it stayed idle. A rank with a CPU
+    worker (hybrid engine, -C 1) gives two entries: its GPU, then its CPU worker (ref
+    arrays of commSize * NB_THREADS entries, PFSP_statistic.c:115-167)."""
 
-    def __init__(self, counts, times):
+    def __init__(self, counts, times, hybrid: bool = False):
         super().__init__()
-        self._src = (counts, times)
+        self._src = (counts, times, hybrid)
 
     def _fill(self):
         if self._src is not None:
-            c, t = self._src
+            c, t, hybrid = self._src
             self._src = None
-            super().extend(WorkerStats(
-                tree=int(c[r, 0]), sol=int(c[r, 1]), gen_child=int(c[r, 0]), steals=int(c[r, 6]),
-                success_steals=int(c[r, 7]), terminations=int(c[r, 8]), t_memcpy=float(t[r, 5]),
-                t_malloc=float(t[r, 6]), t_kernel=float(t[r, 0]), t_pool_ops=float(t[r, 1]), t_idle=float(t[r, 2]),
-                t_termination=float(t[r, 3]), t_load_bal=float(t[r, 4]), dist_load_bal=int(c[r, 4]))
-                for r in range(len(c)))
+            for r in range(len(c)):
+                ct, cs = (int(c[r, 11]), int(c[r, 12])) if c.shape[1] > 12 else (0, 0)
+                super().append(WorkerStats(
+                    tree=int(c[r, 0]) - ct, sol=int(c[r, 1]) - cs, gen_child=int(c[r, 0]) - ct, steals=int(c[r, 6]),
+                    success_steals=int(c[r, 7]), terminations=int(c[r, 8]), t_memcpy=float(t[r, 5]),
+                    t_malloc=float(t[r, 6]), t_kernel=float(t[r, 0]), t_pool_ops=float(t[r, 1]),
+                    t_idle=float(t[r, 2]), t_termination=float(t[r, 3]), t_load_bal=float(t[r, 4]),
+                    dist_load_bal=int(c[r, 4])))
+                if hybrid:
+                    super().append(WorkerStats(tree=ct, sol=cs, gen_child=ct))
 
     def __len__(self):
         self._fill()
@@ -337,7 +349,7 @@ class DistSolver:
         out = self._s.outcome()
         cnt, tms = out["counts"], out["times"]
         return SolveResult(best=int(best), tree=int(tree), sol=int(sol), elapsed=elapsed, t_init=t_init,
-                           t_search=t_search, t_tail=0.0, workers=RankTable(cnt, tms),
+                           t_search=t_search, t_tail=0.0, workers=RankTable(cnt, tms, bool(self.cfg.cpu_workers)),
                            extra={"rounds": int(rounds), "sent_nodes": cnt[:, 2].tolist(),
                                   "received_nodes": cnt[:, 3].tolist(), "world": self.comm.world,
                                   "complete": bool(complete), "dropped_transfers": int(cnt[:, 10].sum()),

@@ -33,6 +33,9 @@ def solve_rank(spec: dict) -> dict:
             pin_to_device(device)
         engine = model.make_engine(backend, device, opts)
         cfg = DistConfig(**spec.get("dist", {}))
+        if cfg.cpu_workers > 0:  # a CPU worker next to the rank's engine (ref -C 1)
+            engine = model.make_hybrid(engine, backend, cfg.cpu_workers, m=cfg.m, cap=4 * cfg.cpu_batch,
+                                       batch=cfg.cpu_batch)
         res = None
         window = opts.max_parents if backend == "gpu" else None
         solver = DistSolver(model, engine, comm, cfg, window=window) if spec.get("session") else None

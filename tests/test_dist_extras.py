@@ -117,3 +117,30 @@ def test_bench_extras_failure_still_prints_headline():
     assert out.returncode == 0, out.stderr[-2000:]
     rec = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][0])
     assert rec["value"] > 0 and rec["extras"]["nosuch"] == {"error": "unknown extra"}
+
+
+@pytest.mark.parametrize("world,problem", [(1, "pfsp"), (2, "pfsp"), (2, "nqueens")])
+def test_cpu_worker_per_rank(world, problem, tmp_path):
+    # -C 1 in the process-per-rank runtime: every rank's engine is a hybrid of its main
+    # engine and a CPU worker thread (csrc/core/hybrid_engine.hpp); golden tree, and the
+    # CPU workers explore part of it (two workers per rank in the statistics)
+    spec = {"problem": problem, "inst": 14, "lb": 1, "N": 11, "backend": "cpu", "session": True, "repeat": 2,
+            "engine": {"cpu_batch": 64},
+            "dist": {"cpu_workers": 2, "cpu_batch": 64, "m": 8, "init_per_rank": 16}}
+    res = spawn_local(world, solve_rank, (spec,), timeout=300)
+    gold = GOLD if problem == "pfsp" else (166925, 2680, None)
+    for r in res:
+        assert (r["tree"], r["sol"]) == gold[:2]
+    ws = res[0]["workers"]
+    assert len(ws) == 2 * world
+    assert sum(w["tree"] for w in ws) + 0 <= gold[0]
+    assert all(ws[2 * k + 1]["tree"] > 0 for k in range(world)), ws  # every CPU worker took part
+    from dist_gpu_accelerated_tree_search_amd.utils import report
+
+    workers = [report.WorkerStats(**w) for w in ws]
+    path = tmp_path / "dist_multigpu.csv"
+    report.write_dist_multi_gpu_csv(str(path), 14, 1, 1, 1, 1, world, res[0]["best"] or 0, 8, 50000, 64,
+                                    res[0]["elapsed"], res[0]["tree"], res[0]["sol"], workers,
+                                    [w.dist_load_bal for w in workers], [w.t_load_bal for w in workers])
+    row = path.read_text().splitlines()[1]
+    assert row.count("[") >= 10 and row.endswith(",")
