@@ -44,6 +44,15 @@ struct EngineStats {
   unsigned long long cpu_tree = 0, cpu_sol = 0;
 };
 
+// Device staging buffers for GPU -> GPU transfers (implemented by the HIP side,
+// csrc/hip/host_support.hpp HipStaging).
+class DeviceStaging {
+ public:
+  virtual ~DeviceStaging() = default;
+  virtual void* alloc(int device, size_t bytes) = 0;
+  virtual void release(int device, void* p) = 0;
+};
+
 // Type-erased interface used by the Python bindings and the native CLIs.
 class IEngine {
  public:

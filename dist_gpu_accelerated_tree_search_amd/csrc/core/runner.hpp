@@ -94,14 +94,6 @@ struct WorkerReport {
   bool pinned = false;
 };
 
-// Device staging buffers for GPU -> GPU transfers (implemented by the HIP side).
-class DeviceStaging {
- public:
-  virtual ~DeviceStaging() = default;
-  virtual void* alloc(int device, size_t bytes) = 0;
-  virtual void release(int device, void* p) = 0;
-};
-
 class RoundBarrier {
  public:
   explicit RoundBarrier(int n) : n_(n) {}

@@ -12,6 +12,7 @@
 #include "../core/cpu_engine.hpp"
 #include "../core/drivers_cpu.hpp"
 #include "../core/hybrid_engine.hpp"
+#include "../core/multi_engine.hpp"
 #include "../core/runner.hpp"
 
 using namespace tts;
@@ -110,6 +111,23 @@ int main() {
     while (h.size() > 0) h.run(-1, 0.002, 1);
     const EngineStats st = h.stats();
     CHECK(st.tree == seq_ub.tree && st.sol == seq_ub.sol);
+  }
+  {  // several sub-engines run concurrently as one engine, steal-half between slices
+    CpuEngine<PfspFrontProblem<5>> a(PfspFrontProblem<5>(in, 0), 16, 1), b(PfspFrontProblem<5>(in, 0), 16, 1),
+        c(PfspFrontProblem<5>(in, 0), 16, 1);
+    MultiConfig mc2;
+    mc2.needy_below = 8;
+    mc2.donor_min = 32;
+    MultiEngine me({&a, &b, &c}, nullptr, mc2);
+    const auto root = PfspFrontProblem<5>(in, 0).root();
+    const EngineStats st = me.solve_from(&root, 1, seq.best);
+    std::printf("multi: tree %llu sol %llu best %d hand-overs %llu\n", st.tree, st.sol, st.best, me.handovers());
+    CHECK(st.tree == seq_ub.tree && st.sol == seq_ub.sol && st.best == seq.best);
+    CHECK(me.handovers() > 0);
+    me.begin(&root, 1, seq.best);
+    while (me.size() > 0) me.run(-1, 0.001, 1);
+    const EngineStats s2 = me.stats();
+    CHECK(s2.tree == seq_ub.tree && s2.sol == seq_ub.sol);
   }
   std::printf(failures ? "SELFTEST FAILED\n" : "SELFTEST OK\n");
   return failures ? 1 : 0;

@@ -11,7 +11,7 @@ import numpy as np
 
 from .. import ops
 from ..utils import nodes as nodes_mod
-from .pfsp import EngineOptions
+from .pfsp import EngineOptions, make_multi
 
 
 class QueensModel:
@@ -43,6 +43,8 @@ class QueensModel:
 
     def make_engine(self, backend: str = "gpu", device: int = 0, opts: EngineOptions | None = None):
         opts = opts or EngineOptions(max_parents=1 << 20)
+        if opts.streams > 1:
+            return make_multi(self, backend, device, opts)
         if backend == "cpu":
             return ops.cpu().make_queens_cpu_engine(self.N, self.G, opts.cpu_batch, opts.cpu_threads)
         if backend != "gpu":

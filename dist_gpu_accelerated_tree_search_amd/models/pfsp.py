@@ -37,6 +37,24 @@ class EngineOptions:
     use_graphs: bool = True
     cpu_batch: int = 4096           # CPU engine batch
     cpu_threads: int = 1
+    # sub-engines per device, one stream and host thread each, run as one engine
+    # (csrc/core/multi_engine.hpp): large trees fill the GPU better (ta021 LB1_d 15.5 s
+    # with 1, 9.9 s with 2, 9.1 s with 3 engines, profiles/r3/concurrency_probe.txt);
+    # the ring is shared out between them. 1: a plain engine (latency-bound small trees)
+    streams: int = 1
+
+
+def make_multi(model, backend: str, device: int, opts: EngineOptions):
+    """opts.streams engines of `model` on one device as one engine (ring shared out;
+    sub-engines below a quarter of a parent window take half of the largest pool)."""
+    from dataclasses import replace
+
+    k = int(opts.streams)
+    sub = replace(opts, streams=1, ring_bytes=max(1 << 26, opts.ring_bytes // k))
+    engines = [model.make_engine(backend, device, sub) for _ in range(k)]
+    mod = ops.hip() if backend == "gpu" else ops.cpu()
+    window = opts.max_parents if backend == "gpu" else opts.cpu_batch
+    return mod.make_multi_engine(engines, max(1, window // 4), max(2, window))
 
 
 class PfspModel:
@@ -110,6 +128,8 @@ class PfspModel:
     # ---- engines ----
     def make_engine(self, backend: str = "gpu", device: int = 0, opts: EngineOptions | None = None):
         opts = opts or EngineOptions()
+        if opts.streams > 1:
+            return make_multi(self, backend, device, opts)
         if backend == "cpu":
             return ops.cpu().make_pfsp_cpu_engine(self.native, self.lb, opts.cpu_batch, opts.cpu_threads)
         if backend != "gpu":

@@ -144,3 +144,32 @@ def test_cpu_worker_per_rank(world, problem, tmp_path):
                                     [w.dist_load_bal for w in workers], [w.t_load_bal for w in workers])
     row = path.read_text().splitlines()[1]
     assert row.count("[") >= 10 and row.endswith(",")
+
+
+@pytest.mark.parametrize("streams", [2, 3])
+def test_multi_engine_cpu_golden(streams):
+    # several sub-engines as one engine (csrc/core/multi_engine.hpp): concurrent slices,
+    # steal-half between them; repeated solves and time slices keep the golden tree
+    from dist_gpu_accelerated_tree_search_amd.models.pfsp import EngineOptions, PfspModel
+    from dist_gpu_accelerated_tree_search_amd.search import solve_engine
+
+    model = PfspModel(14, 1)
+    eng = model.make_engine("cpu", 0, EngineOptions(streams=streams, cpu_batch=64))
+    for _ in range(2):
+        r = solve_engine(model, eng)
+        assert (r.tree, r.sol, r.best) == GOLD
+    nodes, t1, s1, best = model.warmup(1377, 25)
+    eng.begin(nodes, best)
+    while eng.size() > 0:
+        eng.run(max_seconds=0.003)
+    st = eng.stats()
+    assert (st["tree"] + t1, st["sol"] + s1) == GOLD[:2]
+
+
+def test_multi_engine_in_session():
+    # a rank engine made of sub-engines inside the distributed session (2 ranks)
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu", "session": True, "repeat": 2,
+            "engine": {"streams": 2, "cpu_batch": 128}}
+    res = spawn_local(2, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == GOLD

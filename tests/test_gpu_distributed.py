@@ -82,3 +82,47 @@ def test_gpu_unknown_optimum_multi_rank(live):
             "ub": 0, "engine": {"ring_bytes": 1 << 30, "max_parents": 1 << 16}, "dist": {"live_best": live}}
     res = spawn_local(2, solve_rank, (spec,), timeout=600)
     assert all(r["best"] == 1377 for r in res)
+
+
+@pytest.mark.parametrize("key,streams", [((14, 1), 2), ((14, 1), 3), ((8, 0), 3)])
+def test_gpu_multi_engine_golden(key, streams):
+    # sub-engines on one GPU (own stream and host thread each) as one engine
+    from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel
+    from dist_gpu_accelerated_tree_search_amd.search import solve_engine
+
+    gold = {(14, 1): (2573652, 2648, 1377), (8, 0): (113458723, 808498, 1206)}[key]
+    model = PfspModel(*key)
+    eng = model.make_engine("gpu", 0, EngineOptions(streams=streams, ring_bytes=3 << 30, max_parents=1 << 16))
+    for _ in range(2):
+        r = solve_engine(model, eng)
+        assert (r.tree, r.sol, r.best) == gold
+
+
+def test_gpu_multi_engine_queens():
+    from dist_gpu_accelerated_tree_search_amd import EngineOptions, QueensModel
+    from dist_gpu_accelerated_tree_search_amd.search import solve_engine
+
+    model = QueensModel(13, 1)
+    eng = model.make_engine("gpu", 0, EngineOptions(streams=2, ring_bytes=1 << 29, max_parents=1 << 14))
+    r = solve_engine(model, eng)
+    assert (r.tree, r.sol) == (4674889, 73712)
+
+
+def test_gpu_multi_engine_ranks():
+    # 2 ranks, each rank engine = 2 sub-engines (4 engines on one GPU), native session
+    spec = {"problem": "pfsp", "inst": 14, "lb": 1, "backend": "gpu", "comm": "gloo", "device": 0, "session": True,
+            "repeat": 2, "engine": {"ring_bytes": 1 << 29, "max_parents": 1 << 15, "streams": 2}}
+    res = spawn_local(2, solve_rank, (spec,), timeout=600)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == (2573652, 2648, 1377)
+
+
+def test_gpu_cpu_worker_per_rank():
+    # -C 1 under the process-per-GPU runtime: GPU engine + CPU worker per rank
+    spec = {"problem": "pfsp", "inst": 14, "lb": 1, "backend": "gpu", "comm": "gloo", "device": 0, "session": True,
+            "repeat": 2, "engine": {"ring_bytes": 1 << 29, "max_parents": 1 << 14},
+            "dist": {"cpu_workers": 2, "cpu_batch": 256}}
+    res = spawn_local(2, solve_rank, (spec,), timeout=600)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == (2573652, 2648, 1377)
+    assert len(res[0]["workers"]) == 4
