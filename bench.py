@@ -97,6 +97,9 @@ def main() -> int:
     ap.add_argument("--extra-inst-lb1d", type=int, default=21, help=argparse.SUPPRESS)
     ap.add_argument("--extra-inst-lb2", type=int, default=56, help=argparse.SUPPRESS)
     ap.add_argument("--extra-ring-gb", type=float, default=64.0)
+    ap.add_argument("--extra-streams", type=int, default=3,
+                    help="engines per GPU for the extras (csrc/core/multi_engine.hpp; 1 = one engine)")
+    ap.add_argument("--extra-max-parents", type=int, default=1 << 19)
     a = ap.parse_args()
     out = Emitter()  # before anything can write to stdout
 
@@ -223,7 +226,9 @@ def run_solve_extra(a, comm, device: int, inst: int, lb: int, time_limit: float)
     from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig, DistSolver
 
     model = PfspModel(inst, lb)
-    opts = EngineOptions(ring_bytes=int(a.extra_ring_gb * (1 << 30)))
+    # big trees: several engines per GPU fill it better than one (profiles/r3/streams*.txt)
+    opts = EngineOptions(ring_bytes=int(a.extra_ring_gb * (1 << 30)), streams=max(1, a.extra_streams),
+                         max_parents=a.extra_max_parents)
     t_setup = time.perf_counter()
     engine = model.make_engine(a.backend, device, opts)
     cfg = DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws, time_limit_s=time_limit)
@@ -239,7 +244,7 @@ def run_solve_extra(a, comm, device: int, inst: int, lb: int, time_limit: float)
     d = {"config": name, "n_gpus": comm.world, "seconds": dt, "tree": r.tree, "sol": r.sol, "makespan": r.best,
          "nodes_per_s": r.tree / dt, "complete": bool(r.extra.get("complete", True)),
          "rounds": r.extra.get("rounds"), "per_rank_tree": [w.tree for w in r.workers],
-         "engine_setup_s": t_setup}
+         "engine_setup_s": t_setup, "engines_per_gpu": max(1, a.extra_streams), "max_parents": opts.max_parents}
     if time_limit > 0:
         d["time_box_s"] = time_limit
     else:

@@ -5,12 +5,18 @@
 
 pfsp:  -D 0            CPU only: -C threads (0/1 = sequential, ref pfsp_c / pfsp_omp_c)
        -D 1            one GPU (ref pfsp_multigpu_cuda.out -D 1)
-       -D N            N GPUs, one process per GPU (ranks spawned here, or run the
-                       same command under torchrun); -w / -L enable work sharing
-                       inside a node / across nodes (ref -w, -L).
-       -C 1 (D >= 1)   add a CPU worker next to the GPUs (ref -C 1); runs the
-                       single-process native runner (one host thread per GPU,
-                       xGMI peer steals), as does --single-process.
+       -D N            N GPUs. Routing:
+                         -C 1 (the default, ref -C 1), no torchrun: ONE process drives
+                           every GPU plus a CPU worker (native runner, one host thread
+                           per GPU, xGMI peer steals: ref pfsp_multigpu_cuda), as does
+                           --single-process;
+                         -C 0, no torchrun: one process per GPU, spawned here
+                           (RCCL between them: ref pfsp_dist_multigpu_cuda layout);
+                         under torchrun: one process per GPU, with -C 1 each rank also
+                           runs a CPU worker thread (hybrid rank engine, ref -C 1 of
+                           the distributed driver).
+                       -w / -L enable work sharing inside a node / across nodes.
+       --streams K     K engines per GPU, run concurrently (large trees).
 nqueens: -D 0 CPU sequential (ref nqueens_c), -D >= 1 GPU(s).
 Results: the reference's stdout blocks, plus a CSV row (singlegpu.csv,
 multigpu.csv or dist_multigpu.csv) and optionally a JSON record (--json).
@@ -50,6 +56,8 @@ def _pfsp_parser() -> argparse.ArgumentParser:
                     help="minimum local search between coordination rounds, ms (adaptive up to 50 ms)")
     ap.add_argument("--pin", type=int, default=1, help="pin GPU host threads to the GPU's NUMA node")
     ap.add_argument("--ring-gb", type=float, default=16.0)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="engines per GPU, one stream and host thread each, run as one (large trees: 3)")
     ap.add_argument("--json", default=None, help="append a JSON run record to this file")
     ap.add_argument("--csv-dir", default=".", help="directory of the CSV statistics files")
     ap.add_argument("--no-csv", action="store_true")
@@ -92,11 +100,15 @@ def _steal_cap(a) -> int:
     return a.steal_cap if a.steal_cap else 5 * a.M
 
 
-def _rank_spec(a) -> dict:
+def _rank_spec(a, world: int = 1) -> dict:
+    # -C 1 under torchrun: a CPU worker thread per rank (ref NB_THREADS_GPU - 1 threads)
+    cpu = max(1, _cpu_worker_threads(world) // max(1, world)) if a.C == 1 else 0
     return {"problem": "pfsp", "inst": a.inst, "lb": a.lb, "ub": a.ub, "backend": "gpu",
-            "engine": {"max_parents": a.max_parents, "ring_bytes": int(a.ring_gb * (1 << 30))},
+            "engine": {"max_parents": a.max_parents, "ring_bytes": int(a.ring_gb * (1 << 30)),
+                       "streams": max(1, a.streams)},
             "dist": {"m": a.m, "init_per_rank": a.m, "steal_cap": _steal_cap(a), "ws": bool(a.ws), "L": bool(a.L),
-                     "slice_min_s": a.comm_period * 1e-3}, "pin": bool(a.pin)}
+                     "slice_min_s": a.comm_period * 1e-3, "cpu_workers": max(0, cpu), "cpu_batch": a.T},
+            "pin": bool(a.pin)}
 
 
 def _cpu_worker_threads(n_gpus: int) -> int:
@@ -123,7 +135,7 @@ def _pfsp_single_process(a, model) -> int:
     threads = _cpu_worker_threads(len(devices)) if a.C == 1 else 0
     print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, a.D, a.C, a.ws, 1, a.L, 2))
     opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * 2**30), cpu_batch=a.T,
-                         cpu_threads=max(1, threads))
+                         cpu_threads=max(1, threads), streams=max(1, a.streams))
     r = solve_workers(model, devices=tuple(devices), cpu_threads=threads, ub=a.ub, m=a.m, steal_cap=_steal_cap(a),
                       ws=bool(a.ws), opts=opts, slice_min=a.comm_period * 1e-3, pin=bool(a.pin))
     print(report.phase("Initial search on CPU completed", 0, 0, r.t_init))
@@ -165,7 +177,8 @@ def pfsp_main(argv: list[str]) -> int:
 
     if a.D == 1 and world_env == 1:
         print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, 1, a.C, a.ws, 1, a.L, 2))
-        eng = model.make_engine("gpu", 0, EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * 2**30)))
+        eng = model.make_engine("gpu", 0, EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * 2**30),
+                                                        streams=max(1, a.streams)))
         r = solve_engine(model, eng, ub=a.ub, m=a.m, verbose=True)
         print(report.pfsp_results(r.best, r.tree, r.sol, r.elapsed))
         if not a.no_csv:
@@ -180,7 +193,9 @@ def pfsp_main(argv: list[str]) -> int:
     # ---- several GPUs: one process per GPU ----
     from .parallel.workers import solve_rank
 
-    spec = _rank_spec(a)
+    spec = _rank_spec(a, world_env if world_env > 1 else a.D)
+    if world_env == 1:
+        spec["dist"]["cpu_workers"] = 0  # spawned ranks: -C 0 (with -C 1 this was the native runner)
     if world_env > 1:  # already under torchrun
         res = solve_rank(spec)
         if res["rank"] != 0:

@@ -51,6 +51,10 @@ class DeviceStaging {
   virtual ~DeviceStaging() = default;
   virtual void* alloc(int device, size_t bytes) = 0;
   virtual void release(int device, void* p) = 0;
+  // events for stream ordering between engines (IEngine::record_event / wait_event);
+  // 0 where there is no device
+  virtual uintptr_t make_event(int device) { (void)device; return 0; }
+  virtual void free_event(int device, uintptr_t ev) { (void)device; (void)ev; }
 };
 
 // Type-erased interface used by the Python bindings and the native CLIs.
@@ -71,6 +75,12 @@ class IEngine {
   virtual void import_device(const void* src, size_t n) = 0;
   virtual uintptr_t transfer_stream() const { return 0; }
   virtual void fence() {}
+  // Ordering between engines without host waits (GPU engines; no-ops elsewhere):
+  // record_event marks everything enqueued so far on the compute stream, wait_event
+  // makes the compute stream wait for an event recorded by another engine (possibly
+  // on another device). Events come from DeviceStaging::make_event.
+  virtual void record_event(uintptr_t ev) { (void)ev; }
+  virtual void wait_event(uintptr_t ev) { (void)ev; }
   virtual void set_progress_hook(ProgressHook hook) { (void)hook; }
   // Sum over the pool of w[depth] (clamped to the last entry): with w[d] the share
   // of the search space below a node of depth d, 1 - pool_weight is the explored

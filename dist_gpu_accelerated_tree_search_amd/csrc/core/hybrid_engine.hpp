@@ -50,6 +50,8 @@ class HybridEngine final : public IEngine {
   uintptr_t stream() const override { return g_->stream(); }
   int device() const override { return g_->device(); }
   void fence() override { g_->fence(); }
+  void record_event(uintptr_t ev) override { g_->record_event(ev); }
+  void wait_event(uintptr_t ev) override { g_->wait_event(ev); }
   void synchronize() override { g_->synchronize(); }
   void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
 

@@ -81,6 +81,11 @@ class MultiEngine final : public IEngine {
   void fence() override {
     for (auto* x : e_) x->fence();
   }
+  // exports from other sub-engines are fenced (export_device), imports go to sub-engine 0
+  void record_event(uintptr_t ev) override { e_[0]->record_event(ev); }
+  void wait_event(uintptr_t ev) override {
+    for (auto* x : e_) x->wait_event(ev);
+  }
   void synchronize() override {
     for (auto* x : e_) x->synchronize();
   }
@@ -242,10 +247,33 @@ class MultiEngine final : public IEngine {
       }
       return end_.load(std::memory_order_acquire);
     });
-    const long l = x->run(-1, left, 1);
+    // Leave the replay loop below needy_below nodes while another sub-engine can
+    // donate (it is then asked for work at once), else run the pool down to empty.
+    using clock = std::chrono::steady_clock;
+    const auto t0 = clock::now();
+    auto remaining = [&]() -> double {
+      if (left <= 0) return 0.0;
+      return std::max(1e-6, left - std::chrono::duration<double>(clock::now() - t0).count());
+    };
+    auto can_donate = [&]() {
+      for (size_t k = 0; k < e_.size(); ++k)
+        if (static_cast<int>(k) != i && sizes_[k].load(std::memory_order_relaxed) >= cfg_.donor_min) return true;
+      return false;
+    };
+    long l = 0;
+    size_t s = 0;
+    for (;;) {
+      l += x->run(-1, remaining(), can_donate() ? cfg_.needy_below : 1);
+      s = x->size();
+      sizes_[i].store(s, std::memory_order_relaxed);
+      if (end_.load(std::memory_order_acquire) || s == 0) break;
+      if (left > 0 && std::chrono::duration<double>(clock::now() - t0).count() >= left) break;
+      if (s < cfg_.needy_below && can_donate()) {
+        end_.store(true, std::memory_order_release);
+        break;
+      }
+    }
     x->set_progress_hook(nullptr);
-    const size_t s = x->size();
-    sizes_[i].store(s, std::memory_order_relaxed);
     running_.fetch_sub(1, std::memory_order_acq_rel);
     // dry: watch the others' live pool sizes and end the slice as soon as one of them
     // can donate (it stops at its next replay boundary), or until they are all done

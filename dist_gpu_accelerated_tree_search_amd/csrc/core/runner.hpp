@@ -140,8 +140,12 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
   std::vector<int> bests(W, best);
   std::vector<std::vector<uint8_t>> staging_host(W);  // staging_host[r]: nodes bound for worker r
   // device staging: dbuf[r] on worker r's device, written by its (single) donor
-  std::vector<void*> dbuf(W, nullptr);
+  std::vector<void*> dbuf;
   std::vector<size_t> dcap(W, 0), dcount(W, 0);
+  std::vector<int> donor_of(W, -1);
+  std::vector<std::atomic<unsigned long long>> ready(W);  // round whose transfer to worker r is enqueued
+  for (auto& x : ready) x.store(0);
+  std::vector<uintptr_t> ready_ev, done_ev;                // [donor * W + receiver] on the donor's device / [receiver]
   std::vector<std::tuple<int, int, size_t>> plan;
   auto per = [&](const std::vector<size_t>& v, size_t dflt) {
     std::vector<size_t> out(W, dflt);
@@ -150,6 +154,25 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
   };
   const std::vector<size_t> needy = per(cfg.needy_below, cfg.m), donor = per(cfg.donor_min, 2 * cfg.m),
                             rcap = per(cfg.recv_cap, cfg.steal_cap);
+  // device staging and events, allocated once: a receiving GPU gets a buffer for its
+  // largest transfer (recv cap); pairs of GPU workers get an event each way
+  bool any_gpu_pair = false;
+  for (int x = 0; x < W; ++x)
+    for (int y = 0; y < W; ++y) any_gpu_pair |= x != y && engines[x]->device() >= 0 && engines[y]->device() >= 0;
+  if (staging && any_gpu_pair && cfg.work_sharing) {
+    dbuf.assign(W, nullptr);
+    ready_ev.assign(static_cast<size_t>(W) * W, 0);
+    done_ev.assign(W, 0);
+    for (int x = 0; x < W; ++x) {
+      if (engines[x]->device() < 0) continue;
+      dcap[x] = std::min<size_t>(rcap[x], (size_t(1) << 30) / std::max<size_t>(1, nb)) * nb;
+      dbuf[x] = staging->alloc(engines[x]->device(), dcap[x]);
+      done_ev[x] = staging->make_event(engines[x]->device());
+      for (int y = 0; y < W; ++y)
+        if (y != x && engines[y]->device() >= 0)
+          ready_ev[static_cast<size_t>(y) * W + x] = staging->make_event(engines[y]->device());
+    }
+  }
   bool done = false;
   int gbest = best;
   std::vector<std::atomic<size_t>> live(W);
@@ -317,28 +340,28 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
       if (needy_w) ++r.steals;
       if (gbest < bests[w]) guarded([&] { e->set_best(gbest); });
       if (!plan.empty()) {
+        // Only the workers named in the plan take part; the others go straight on to
+        // their next slice. A donor enqueues the copy of its pool bottom into the
+        // receiver's staging buffer (device staging on the receiver's GPU when both
+        // ends are GPUs, peer copy over xGMI; host staging otherwise), records an event
+        // and publishes the count; the receiver's stream waits on that event before
+        // its import, and the donor of a later round waits on the receiver's "import
+        // done" event before it overwrites the buffer. No host sync on either side.
+        const unsigned long long round_id = r.rounds;
         beat(w, Phase::Transfer);
         TTS_RANGE("tts.transfer");
-        // donors: pool bottom -> receiver (device staging on the receiver's GPU
-        // when both ends are GPUs, host staging otherwise)
         for (const auto& t : plan) {
           const int d = std::get<0>(t), rc = std::get<1>(t);
           const size_t k = std::get<2>(t);
           if (d != w) continue;
-          const bool on_device = staging && e->device() >= 0 && engines[rc]->device() >= 0;
+          const bool on_device = !dbuf.empty() && dbuf[rc] && e->device() >= 0;
           size_t got = 0;
           if (on_device) {
             guarded([&] {
-              if (dcap[rc] < k * nb) {
-                if (dbuf[rc]) staging->release(engines[rc]->device(), dbuf[rc]);
-                dbuf[rc] = nullptr;
-                dbuf[rc] = staging->alloc(engines[rc]->device(), k * nb);
-                dcap[rc] = k * nb;
-              }
-              got = e->export_device(dbuf[rc], k);
-              e->fence();  // stream-ordered copy: done before the receiver's barrier
+              e->wait_event(done_ev[rc]);  // the receiver's previous import has read the buffer
+              got = e->export_device(dbuf[rc], std::min(k, dcap[rc] / nb));
+              e->record_event(ready_ev[static_cast<size_t>(d) * W + rc]);
             });
-            dcount[rc] = got;
             ++r.device_transfers;
           } else {
             std::vector<uint8_t> buf(k * nb);
@@ -347,40 +370,52 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
             std::lock_guard<std::mutex> lk(stage_mu);
             staging_host[rc].insert(staging_host[rc].end(), buf.begin(), buf.end());
           }
+          dcount[rc] = on_device ? got : 0;
+          donor_of[rc] = d;
+          ready[rc].store(round_id, std::memory_order_release);
           r.sent += got;
           ++r.transfers_out;
         }
-        beat(w, Phase::Barrier);
-        bar.wait();
-        beat(w, Phase::Transfer);
-        size_t in = 0;
-        if (dcount[w]) {
-          // the copy out of dbuf[w] completes before the round ends: a later round's
-          // donor may overwrite dbuf[w] as soon as it passes the next barrier
-          guarded([&] {
-            e->import_device(dbuf[w], dcount[w]);
-            e->fence();
-          });
-          in += dcount[w];
-          dcount[w] = 0;
+        bool receiving = false;
+        for (const auto& t : plan) receiving |= std::get<1>(t) == w;
+        if (receiving) {
+          // wait until the donor has enqueued its copy (not until it completed)
+          while (ready[w].load(std::memory_order_acquire) != round_id) std::this_thread::yield();
+          size_t in = 0;
+          if (dcount[w]) {
+            const int d = donor_of[w];
+            guarded([&] {
+              e->wait_event(ready_ev[static_cast<size_t>(d) * W + w]);
+              e->import_device(dbuf[w], dcount[w]);
+              e->record_event(done_ev[w]);
+            });
+            in += dcount[w];
+            dcount[w] = 0;
+          }
+          {
+            std::vector<uint8_t> host;
+            {
+              std::lock_guard<std::mutex> lk(stage_mu);
+              host.swap(staging_host[w]);
+            }
+            if (!host.empty()) {
+              guarded([&] { e->push_host(host.data(), host.size() / nb); });
+              in += host.size() / nb;
+            }
+          }
+          if (in) {
+            r.received += in;
+            ++r.transfers_in;
+          }
+          if (needy_w) {
+            if (in)
+              ++r.success_steals;
+            else
+              ++r.idle_rounds;
+          }
+        } else if (needy_w) {
+          ++r.idle_rounds;
         }
-        if (!staging_host[w].empty()) {
-          guarded([&] { e->push_host(staging_host[w].data(), staging_host[w].size() / nb); });
-          in += staging_host[w].size() / nb;
-          staging_host[w].clear();
-        }
-        if (in) {
-          r.received += in;
-          ++r.transfers_in;
-        }
-        if (needy_w) {
-          if (in)
-            ++r.success_steals;
-          else
-            ++r.idle_rounds;
-        }
-        beat(w, Phase::Barrier);
-        bar.wait();
       }
       if (plan.empty() && needy_w) ++r.idle_rounds;
       if (sizes[w] == 0) {
@@ -400,9 +435,15 @@ inline std::vector<WorkerReport> run_workers(const std::vector<IEngine*>& engine
   for (auto& t : th) t.join();
   finished = true;
   if (watchdog.joinable()) watchdog.join();
-  if (staging)
-    for (int w = 0; w < W; ++w)
-      if (dbuf[w]) staging->release(engines[w]->device(), dbuf[w]);
+  if (staging) {
+    for (int x = 0; x < W; ++x) engines[x]->fence();  // imports may still read the staging buffers
+    for (int x = 0; x < static_cast<int>(dbuf.size()); ++x)
+      if (dbuf[x]) staging->release(engines[x]->device(), dbuf[x]);
+    for (int x = 0; x < static_cast<int>(done_ev.size()); ++x)
+      if (done_ev[x]) staging->free_event(engines[x]->device(), done_ev[x]);
+    for (size_t i = 0; i < ready_ev.size(); ++i)
+      if (ready_ev[i]) staging->free_event(engines[i / W]->device(), ready_ev[i]);
+  }
   if (err) std::rethrow_exception(err);
   rep[0].watchdog_events = watchdog_events.load();
   best = gbest;

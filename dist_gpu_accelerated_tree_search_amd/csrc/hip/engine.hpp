@@ -74,6 +74,10 @@ class DeviceEngine final : public IEngine {
     // control-block upload, followed by a pinned staging area for begin()'s nodes (a
     // pageable source would make the node copy synchronous and staged by the runtime)
     TTS_HIP_CHECK(hipHostMalloc(&h_up_, kUpBytes + kStageNodes * sizeof(Node), hipHostMallocDefault));
+    // begin()'s staging, read by the load kernel through its device mapping
+    TTS_HIP_CHECK(hipHostMalloc(&h_begin_, kUpBytes + kStageNodes * sizeof(Node),
+                                hipHostMallocMapped | hipHostMallocCoherent));
+    TTS_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_begin_), h_begin_, 0));
     for (int m = 0; m < 2; ++m) {
       TTS_HIP_CHECK(
           hipHostMalloc(&h_mirror_[m], sizeof(dev::PoolCtl), hipHostMallocMapped | hipHostMallocCoherent));
@@ -169,6 +173,7 @@ class DeviceEngine final : public IEngine {
     (void)hipFree(d_ctl_);
     (void)hipHostFree(h_ctl_);
     (void)hipHostFree(h_up_);
+    (void)hipHostFree(h_begin_);
     for (int m = 0; m < 2; ++m) {
       (void)hipHostFree(h_mirror_[m]);
       (void)hipEventDestroy(graph_done_[m]);
@@ -184,6 +189,16 @@ class DeviceEngine final : public IEngine {
   uintptr_t stream() const override { return reinterpret_cast<uintptr_t>(stream_); }
   uintptr_t transfer_stream() const override { return reinterpret_cast<uintptr_t>(xfer_); }
   void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
+  void record_event(uintptr_t ev) override {
+    if (!ev) return;
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    TTS_HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(ev), stream_));
+  }
+  void wait_event(uintptr_t ev) override {
+    if (!ev) return;
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    TTS_HIP_CHECK(hipStreamWaitEvent(stream_, reinterpret_cast<hipEvent_t>(ev), 0));
+  }
   void fence() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -303,6 +318,7 @@ class DeviceEngine final : public IEngine {
     const auto t0 = std::chrono::steady_clock::now();
     auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
     long launches = 0;
+    bool hook_stopped = false;
     sync_ctl();
     for (;;) {
       // ---- nothing in flight on the compute stream: the host shadow is the device state ----
@@ -321,6 +337,7 @@ class DeviceEngine final : public IEngine {
       if (all < stop_below) break;
       if (max_launches >= 0 && launches >= max_launches) break;
       if (max_seconds > 0 && elapsed() >= max_seconds) break;
+      if (hook_stopped) break;  // the hook asked to stop during the last pipelined stretch
       if (hook_) {
         int b = h_ctl_->best.v;
         const bool stop = hook_(all, b);
@@ -377,8 +394,10 @@ class DeviceEngine final : public IEngine {
       // sync + launch gap between replays. ----
       size_t known = total;
       size_t inflight_growth = static_cast<size_t>((kf ? kf : ks_[gi]) + 1) * buf_nodes_;
+      bool hook_stop = false;
       while (!inflight_.empty()) {
-        const bool budget_ok = (max_launches < 0 || launches < max_launches) && (max_seconds <= 0 || elapsed() < max_seconds);
+        const bool budget_ok = !hook_stop && (max_launches < 0 || launches < max_launches) &&
+                               (max_seconds <= 0 || elapsed() < max_seconds);
         if (inflight_.size() == 1 && budget_ok && known >= spec_min_) {
           const int g2 = pick_graph(known, inflight_growth);
           if (g2 >= 0) {
@@ -391,7 +410,21 @@ class DeviceEngine final : public IEngine {
         check_overflow();
         known = dev_total();
         inflight_growth = inflight_.empty() ? 0 : static_cast<size_t>(inflight_k_.front() + 1) * buf_nodes_;
+        // a long pipelined stretch still answers the hook (live pool size for siblings
+        // and peers, stop requests); a better incumbent from it is applied once nothing
+        // is in flight, at the top of the outer loop
+        if (hook_ && !inflight_.empty() && !hook_stop) {
+          int b = h_ctl_->best.v;
+          hook_stop = hook_(known + spill_.size() + refill_n_, b);
+          if (b < pending_best_) pending_best_ = b;
+        }
       }
+      if (pending_best_ < h_ctl_->best.v) {
+        h_ctl_->best.v = pending_best_;
+        upload_ctl();
+      }
+      pending_best_ = 0x7fffffff;
+      hook_stopped = hook_stop;
     }
     stats_.t_run += elapsed();
     return launches;
@@ -428,14 +461,24 @@ class DeviceEngine final : public IEngine {
     h_ctl_->pend_children = h_ctl_->pend_leaves = h_ctl_->pend_internal = 0;
     h_ctl_->overflow = 0;
     if (n <= kStageNodes) {
-      TTS_HIP_CHECK(hipEventSynchronize(up_done_));  // the previous upload has read the staging area
-      Node* stage = reinterpret_cast<Node*>(reinterpret_cast<char*>(h_up_) + kUpBytes);
+      // one load kernel reads the control block and the nodes from mapped pinned memory
+      if (loader_pending_) TTS_HIP_CHECK(hipStreamSynchronize(stream_));  // it still reads the staging area
+      h_ctl_->slot[0].stack = n;
+      for (auto& sl : h_ctl_->slot) sl.qnext = 0;
+      std::memcpy(h_begin_, h_ctl_, sizeof(dev::PoolCtl));
+      Node* stage = reinterpret_cast<Node*>(reinterpret_cast<char*>(h_begin_) + kUpBytes);
       std::memcpy(stage, nodes, n * sizeof(Node));
-      ring_write_top(stage, n, hipMemcpyHostToDevice);
+      const int blocks = static_cast<int>(std::min<size_t>(64, (n * (sizeof(Node) / 16) + dev::kBlock - 1) / dev::kBlock + 1));
+      hipLaunchKernelGGL(dev::pool_load_kernel<Node>, dim3(blocks), dim3(dev::kBlock), 0, stream_,
+                         reinterpret_cast<const uint32_t*>(d_begin_), d_ctl_,
+                         reinterpret_cast<const uint4*>(reinterpret_cast<char*>(d_begin_) + kUpBytes), d_ring_,
+                         static_cast<dev::u64>(n));
+      TTS_HIP_CHECK(hipGetLastError());
+      loader_pending_ = true;
     } else {
       ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
+      upload_ctl();  // records up_done_ after both copies
     }
-    upload_ctl();  // records up_done_ after both copies
     fresh_ = true;
   }
 
@@ -615,6 +658,7 @@ class DeviceEngine final : public IEngine {
       TTS_HIP_CHECK(hipEventSynchronize(graph_done_[m]));
     }
     std::memcpy(h_ctl_, h_mirror_[m], sizeof(dev::PoolCtl));
+    loader_pending_ = false;  // everything enqueued before that graph has completed
     ++stats_.syncs;
     stats_.t_memcpy += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -886,6 +930,9 @@ class DeviceEngine final : public IEngine {
   dev::PoolCtl* d_ctl_ = nullptr;
   dev::PoolCtl* h_ctl_ = nullptr;
   dev::PoolCtl* h_up_ = nullptr;  // + staging for up to kStageNodes nodes at kUpBytes
+  dev::PoolCtl* h_begin_ = nullptr;  // begin()'s mapped staging (control block + nodes), read by pool_load_kernel
+  dev::PoolCtl* d_begin_ = nullptr;  // ... its device address
+  bool loader_pending_ = false;      // a load kernel may still read h_begin_
   static constexpr size_t kUpBytes = (sizeof(dev::PoolCtl) + 255) & ~size_t(255);
   static constexpr size_t kStageNodes = 4096;
   dev::PoolCtl* h_mirror_[2] = {nullptr, nullptr};
@@ -901,6 +948,7 @@ class DeviceEngine final : public IEngine {
   std::deque<std::pair<hipEvent_t, size_t>> ahead_;
   hipEvent_t refill_ev_ = nullptr;
   ProgressHook hook_;
+  int pending_best_ = 0x7fffffff;  // incumbent handed in by the hook while graphs were in flight
   int next_mirror_ = 0;
   std::deque<int> inflight_, inflight_k_;
   std::deque<dev::u64> inflight_seq_;

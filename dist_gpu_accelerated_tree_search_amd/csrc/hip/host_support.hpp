@@ -52,6 +52,16 @@ class HipStaging final : public DeviceStaging {
     (void)hipSetDevice(device);
     (void)hipFree(p);
   }
+  uintptr_t make_event(int device) override {
+    TTS_HIP_CHECK(hipSetDevice(device));
+    hipEvent_t e = nullptr;
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return reinterpret_cast<uintptr_t>(e);
+  }
+  void free_event(int device, uintptr_t ev) override {
+    (void)hipSetDevice(device);
+    if (ev) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev));
+  }
 };
 
 inline std::string device_pci_bus_id(int device) {

@@ -320,6 +320,23 @@ __global__ __launch_bounds__(kBlock) void pool_flatten_kernel(PoolArgs<Node> pa,
   pool_spill_leftovers<Node, MAXCH, MAXCHUNKS>(pa, v, b, ps);
 }
 
+// Start of a solve (DeviceEngine::begin): the control block and the first nodes are
+// read straight from host-mapped pinned memory — one kernel instead of two copies
+// (each a blit dispatch plus its API call) ahead of the first graph replay. The nodes
+// go to ring[0..n) (begin() resets the ring base).
+template <class Node>
+__global__ __launch_bounds__(kBlock) void pool_load_kernel(const uint32_t* __restrict__ src_ctl, PoolCtl* dctl,
+                                                           const uint4* __restrict__ src_nodes, Node* ring, u64 n) {
+  constexpr int VPN = sizeof(Node) / 16;
+  constexpr int W = static_cast<int>(sizeof(PoolCtl) / 4);
+  const u64 stride = static_cast<u64>(gridDim.x) * kBlock;
+  const u64 tid = static_cast<u64>(blockIdx.x) * kBlock + threadIdx.x;
+  uint32_t* d = reinterpret_cast<uint32_t*>(dctl);
+  for (u64 i = tid; i < static_cast<u64>(W); i += stride) d[i] = src_ctl[i];
+  uint4* dn = reinterpret_cast<uint4*>(ring);
+  for (u64 x = tid; x < n * VPN; x += stride) dn[x] = src_nodes[x];
+}
+
 // Rank share of a replicated pool: out[t] = ring[bot + rank + t*world], t < keep
 // (a strided pick gives every rank a sample of every subtree of the frontier).
 template <class Node>

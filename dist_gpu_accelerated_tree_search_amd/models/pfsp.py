@@ -42,6 +42,11 @@ class EngineOptions:
     # with 1, 9.9 s with 2, 9.1 s with 3 engines, profiles/r3/concurrency_probe.txt);
     # the ring is shared out between them. 1: a plain engine (latency-bound small trees)
     streams: int = 1
+    # sub-engine sharing thresholds in units of the parent window: a sub-engine below
+    # window * stream_needy nodes takes half of a pool of at least window * stream_donor
+    # (same-device copies are cheap: far below the cross-GPU thresholds)
+    stream_needy: float = 1 / 16
+    stream_donor: float = 1 / 4
 
 
 def make_multi(model, backend: str, device: int, opts: EngineOptions):
@@ -54,7 +59,7 @@ def make_multi(model, backend: str, device: int, opts: EngineOptions):
     engines = [model.make_engine(backend, device, sub) for _ in range(k)]
     mod = ops.hip() if backend == "gpu" else ops.cpu()
     window = opts.max_parents if backend == "gpu" else opts.cpu_batch
-    return mod.make_multi_engine(engines, max(1, window // 4), max(2, window))
+    return mod.make_multi_engine(engines, max(1, int(window * opts.stream_needy)), max(2, int(window * opts.stream_donor)))
 
 
 class PfspModel:

@@ -49,6 +49,23 @@ elif which == "spill":  # pinned spill/refill: a ring smaller than the pool (cop
     assert (r.tree, r.sol, r.best) == (2573652, 2648, 1377), (r.tree, r.sol, r.best)
     print(which, "ta014 spilled", st["spilled"], "refilled", st["refilled"], "pinned MB", st["pinned_bytes"] >> 20,
           "capacity", st["capacity"], f"{r.elapsed * 1e3:.1f} ms")
+elif which.startswith("spill021"):  # spill021[:ring_MB[:seconds]]: ta021 LB1_d, 2^14-parent window, small ring
+    parts = which.split(":")
+    ring_mb = int(parts[1]) if len(parts) > 1 else 256
+    box = float(parts[2]) if len(parts) > 2 else 3.0
+    import time
+    m = PfspModel(21, 0)
+    eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 14, ring_bytes=ring_mb << 20))
+    nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
+    eng.begin(nodes, int(best))
+    t0 = time.perf_counter()
+    eng.run(max_seconds=box)
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    print(which, f"ring {ring_mb} MB capacity {st['capacity']} nodes: {st['tree'] / dt / 1e9:.3f} G nodes/s over "
+          f"{dt:.2f} s, spilled {st['spilled']} refilled {st['refilled']} pinned MB {st['pinned_bytes'] >> 20} "
+          f"pool device {st['device_nodes']} host {st['host_nodes']}")
+    raise SystemExit(0)
 elif which == "queens":
     m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=32 << 30))
     r = solve_engine(m, eng)

@@ -25,11 +25,14 @@ def main() -> int:
     ap.add_argument("--streams", default="1,2,3,4")
     ap.add_argument("--box", type=float, default=5.0)
     ap.add_argument("--mp", type=int, default=1 << 19)
+    ap.add_argument("--needy", type=float, default=1 / 16)
+    ap.add_argument("--donor", type=float, default=1 / 4)
     ap.add_argument("--only", default="ta014,ta008,ta021,ta056")
     a = ap.parse_args()
     only = a.only.split(",")
     for k in (int(x) for x in a.streams.split(",")):
-        opts = EngineOptions(streams=k, max_parents=a.mp, ring_bytes=48 << 30)
+        opts = EngineOptions(streams=k, max_parents=a.mp, ring_bytes=48 << 30, stream_needy=a.needy,
+                             stream_donor=a.donor)
         if "ta014" in only:
             m = PfspModel(14, 1)
             eng = m.make_engine("gpu", 0, opts)
@@ -60,7 +63,7 @@ def main() -> int:
             r = solve_engine(m, eng)
             dt = time.perf_counter() - t0
             assert (r.tree, r.sol, r.best) == (260069628524, 14963858, 2297), (r.tree, r.sol, r.best)
-            print(f"streams {k} ta021 LB1_d: {dt:.2f} s -> {r.tree / dt / 1e9:.2f} G nodes/s", flush=True)
+            print(f"streams {k} window {a.mp} needy {a.needy:.4f} donor {a.donor:.4f} ta021 LB1_d: {dt:.2f} s -> {r.tree / dt / 1e9:.2f} G nodes/s", flush=True)
             del eng
         if "ta056" in only:
             m = PfspModel(56, 2)
