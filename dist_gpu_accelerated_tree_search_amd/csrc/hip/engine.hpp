@@ -54,9 +54,20 @@ class DeviceEngine final : public IEngine {
     if (cfg_.max_parents == 0) throw std::invalid_argument("max_parents must be > 0");
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     const auto t0 = std::chrono::steady_clock::now();
-    // the parent window is a whole number of chunks, at most kMaxChunks of them
+    int cus = 0;
+    TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+    cus_ = cus;
+    int per_cu = std::max(1, Traits::blocks_per_cu());
+    if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(g));  // tuning
+    const size_t resident = static_cast<size_t>(cus) * per_cu;
+    // the parent window is a whole number of chunks, at most kMaxChunks of them; with
+    // window_grid, no more chunks than resident workgroups (a window of 2048 chunks on
+    // 1792 resident workgroups runs its last 256 chunks as a second pass)
     const size_t bp = Traits::kParentsPerChunk;
     max_chunks_ = std::min<size_t>((cfg_.max_parents + bp - 1) / bp, Traits::kMaxChunks);
+    bool window_grid = cfg_.window_grid;
+    if (const char* f = std::getenv("TTS_WINDOW_GRID")) window_grid = std::atoi(f) != 0;  // A/B runs
+    if (window_grid) max_chunks_ = std::max<size_t>(1, std::min(max_chunks_, resident));
     cfg_.max_parents = max_chunks_ * bp;
     buf_nodes_ = max_chunks_ * static_cast<size_t>(Traits::kChildrenPerChunk);
     size_t cap = 1;
@@ -116,12 +127,7 @@ class DeviceEngine final : public IEngine {
     if (const char* f = std::getenv("TTS_LOCAL_STEPS")) pa.local_steps = std::min(std::max(0, std::atoi(f)), Traits::kLocalSteps);
     pa.local_min = 0;
     if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
-    int cus = 0;
-    TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
-    cus_ = cus;
-    int per_cu = std::max(1, Traits::blocks_per_cu());
-    if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(g));  // tuning
-    grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, static_cast<size_t>(cus) * per_cu)));
+    grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, resident)));
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known
     // pool spans a whole parent window (spec_min_). Queuing it earlier
@@ -464,7 +470,6 @@ class DeviceEngine final : public IEngine {
       // one load kernel reads the control block and the nodes from mapped pinned memory
       if (loader_pending_) TTS_HIP_CHECK(hipStreamSynchronize(stream_));  // it still reads the staging area
       h_ctl_->slot[0].stack = n;
-      for (auto& sl : h_ctl_->slot) sl.qnext = 0;
       std::memcpy(h_begin_, h_ctl_, sizeof(dev::PoolCtl));
       Node* stage = reinterpret_cast<Node*>(reinterpret_cast<char*>(h_begin_) + kUpBytes);
       std::memcpy(stage, nodes, n * sizeof(Node));
@@ -680,7 +685,6 @@ class DeviceEngine final : public IEngine {
   // so the shadow can be edited again immediately).
   void upload_ctl() {
     TTS_HIP_CHECK(hipEventSynchronize(up_done_));
-    for (auto& sl : h_ctl_->slot) sl.qnext = 0;
     std::memcpy(h_up_, h_ctl_, sizeof(dev::PoolCtl));
     TTS_HIP_CHECK(hipMemcpyAsync(d_ctl_, h_up_, sizeof(dev::PoolCtl), hipMemcpyHostToDevice, stream_));
     TTS_HIP_CHECK(hipEventRecord(up_done_, stream_));

@@ -113,27 +113,25 @@ inline int lb2_pipe_wanted() {
   return f ? (std::atoi(f) != 0) : 1;
 }
 
-// The LB2 kernel with two children per lane in packed u16 walks (LBK 5): every walk
-// value is at most the sum of all processing times, which must fit 16 bits, and job
-// sets must fit one word. On when it applies unless TTS_LB2_PK=0 (A/B).
+// The LB2 kernel with two children per lane in packed u16 walks (LBK 5): job sets
+// must fit one word, and every walk value must fit 16 bits. A walk value (a child
+// front, t0 + p0, t0 + lag, t1 + p1) is the length of a monotone staircase path
+// through the machine x job grid (prefix columns, then Johnson-order columns; a lag
+// is the column segment between the pair's machines), so it visits at most
+// jobs + machines - 1 cells: (jobs + machines - 1) * max p bounds it (50 x 20 with
+// p <= 99: 6,831). The tails are added in 32 bits after the walk. On when it applies
+// unless TTS_LB2_PK=0 (A/B).
 inline bool lb2_pk_ok(const PfspInstance& in) {
   if (in.jobs > 64) return false;
-  long tot = 0;
-  for (int v : in.p) tot += v;
-  return tot < 65536;
+  long pmax = 0;
+  for (int v : in.p) pmax = std::max<long>(pmax, v);
+  return (in.jobs + in.machines - 1) * pmax < 65536;
 }
 inline bool lb2_pk_wanted(const PfspInstance& in) {
   const char* f = std::getenv("TTS_LB2_PK");
   return (f ? std::atoi(f) != 0 : true) && lb2_pk_ok(in);
 }
 
-// Dynamic chunk deal in the LB2 expand kernel: TTS_LB2_DYN=1 (A/B; measured slower
-// than the static deal of strided chunks: the queue atomic's return holds up the
-// chunk's first loads).
-inline int lb2_dyn_wanted() {
-  const char* f = std::getenv("TTS_LB2_DYN");
-  return f ? (std::atoi(f) != 0) : 0;
-}
 // Strided LB2 chunks (parents ch + i * nchunks): on unless TTS_LB2_STRIDE=0 (A/B).
 inline int lb2_stride_wanted() {
   const char* f = std::getenv("TTS_LB2_STRIDE");
@@ -207,7 +205,6 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
   a.npairs = PR;
   a.rs4 = img.rs4;
   a.lb2_pipe = lb2_pipe_wanted();
-  a.lb2_dyn = lb2_dyn_wanted();
   a.lb2_stride = lb2_stride_wanted();
   for (int m = 0; m < M; ++m) {
     if (m < MR) {
@@ -237,29 +234,6 @@ inline PfspTableImages pfsp_fill_args(const PfspInstance& in, dev::PfspArgs<NJ, 
   return img;
 }
 
-// LB2 records fit the packed 4-B LDS layout of kernel LBK 3 ({job:6 | p0:7 | p1:7 | lag:12}).
-inline bool lb2_records_pack(const PfspInstance& in) {
-  if (in.jobs > 64) return false;
-  for (int v : in.p)
-    if (v > 127) return false;
-  for (int v : in.lags)
-    if (v > 4095) return false;
-  return true;
-}
-// The 50-job LB2 kernel with every record in LDS (LBK 3): TTS_LB2_PACK=1 (A/B).
-inline bool lb2_pack_wanted(const PfspInstance& in) {
-  const char* f = std::getenv("TTS_LB2_PACK");
-  return f && std::atoi(f) != 0 && lb2_records_pack(in);
-}
-// The LB2 kernel with prefix/suffix walks per (parent, pair) (LBK 4, lb2_ps_walks):
-// O(N) per (parent, pair) instead of per (child, pair), exact, but measured slower
-// than the per-child walks with the LB1 filter and early exit (ta056 0.082 -> 0.039
-// G nodes/s, ta010 4.3 -> 6.0 ms, profiles/r2/lb2_variants.md): TTS_LB2_PS=1 (A/B).
-inline bool lb2_ps_wanted() {
-  const char* f = std::getenv("TTS_LB2_PS");
-  return f && std::atoi(f) != 0;
-}
-
 template <class T>
 inline T* upload_vec(const std::vector<T>& v) {
   T* d = nullptr;
@@ -277,10 +251,6 @@ std::unique_ptr<IEngine> make_pfsp_engine_t(const PfspInstance& in, const Engine
   a.recs = upload_vec(img.recs);
   a.pinfo = upload_vec(img.pinfo);
   a.recs4 = upload_vec(img.recs4);
-  // wave-uniform pair walks measured 2.6x slower on ta056 (active children per chunk
-  // fill a fraction of a wave, profiles/r1/r1af): dense (pair, child) tasks by default
-  a.lb2_wave = 0;
-  if (const char* f = std::getenv("TTS_LB2_WAVE")) a.lb2_wave = std::atoi(f) != 0;  // A/B runs
   // B2 in rounds of pairs: ta056 (50x20) 0.060 -> 0.081 G nodes/s, ta020 (20x10)
   // 11.1 -> 8.0 ms, ta014 (20x10) even; ta010 (20x5, 10 pairs) 4.0 -> 4.6 ms
   // (profiles/r1/r1ak): on from 10 machines (45 pairs)
@@ -338,9 +308,8 @@ std::vector<int> pfsp_gpu_bounds_t(const PfspInstance& in, const void* parents, 
 // over `n` parents loaded as the window, with the kernel's debug output on. Returns
 // every child's bound in parent order (children k = depth..N-1): the exact LB2 when
 // it is below `best`, otherwise a value >= best (the kernel's prune decision).
-// variant: 0 prefix/suffix walks (kernel LBK 4), 1 rounds of dense walks, 2 dense
-// walks, 3 wave-uniform walks, 4 rounds of packed two-child walks (kernel LBK 5, the
-// default search path where lb2_pk_ok).
+// variant: 1 rounds of dense walks, 2 dense walks, 4 rounds of packed two-child walks
+// (kernel LBK 5, the default search path where lb2_pk_ok).
 // With `timing`: `reps` more launches without the debug output, each from the same
 // window (ring and control block restored), on the engine's grid (resident
 // workgroups), then one launch with the phase timers; timing = {min ms, median ms,
@@ -383,8 +352,8 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
     a.recs4 = up(img.recs4);
     a.dbg_off = up(offsets);
     a.dbg_lb = up(out);
+    if (variant != 1 && variant != 2 && variant != 4) throw std::invalid_argument("expand probe: variant 1, 2 or 4");
     a.lb2_rounds = variant == 1 || variant == 4;
-    a.lb2_wave = variant == 3;
     size_t cap = 1;
     while (cap < n) cap *= 2;
     auto& pa = a.pool;
@@ -406,9 +375,7 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
     pa.max_chunks = static_cast<int>(nchunks);
     if (variant == 4 && !lb2_pk_ok(in)) throw std::invalid_argument("expand probe: packed walks do not apply");
     auto launch = [&](const dim3& grid) {
-      if (variant == 0)
-        hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, 4>), grid, dim3(dev::kBlock), 0, 0, a, 0);
-      else if (variant == 4)
+      if (variant == 4)
         hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, 5>), grid, dim3(dev::kBlock), 0, 0, a, 0);
       else
         hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), grid, dim3(dev::kBlock), 0, 0, a, 0);
@@ -419,10 +386,7 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
     TTS_HIP_CHECK(hipMemcpy(out.data(), a.dbg_lb, nb * sizeof(int), hipMemcpyDeviceToHost));
     if (timing) {
       int bpc = 0, cus = 0;
-      if (variant == 0)
-        TTS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::pfsp_expand_kernel<NJ, M, 4>,
-                                                                   dev::kBlock, 0));
-      else if (variant == 4)
+      if (variant == 4)
         TTS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, dev::pfsp_expand_kernel<NJ, M, 5>,
                                                                    dev::kBlock, 0));
       else
@@ -575,9 +539,6 @@ TTS_PFSP_DECLARE_BUCKET(500)
       if constexpr (NJ == 20)                                                                        \
         if (pfsp_front_ok(in, lb)) return make_pfsp_front_engine_t<M>(in, cfg);                      \
       if (lb != 2) return make_pfsp_engine_t<NJ, M, 1>(in, cfg);                                    \
-      if constexpr (NJ == 50)                                                                        \
-        if (lb2_pack_wanted(in)) return make_pfsp_engine_t<NJ, M, 3>(in, cfg);                       \
-      if (lb2_ps_wanted()) return make_pfsp_engine_t<NJ, M, 4>(in, cfg);                             \
       if constexpr (NJ <= 64)                                                                        \
         if (M >= 10 && lb2_pk_wanted(in)) return make_pfsp_engine_t<NJ, M, 5>(in, cfg);               \
       return make_pfsp_engine_t<NJ, M, 2>(in, cfg);                                                  \

@@ -44,7 +44,7 @@ struct PfspGeom {
   // many workgroups and keep the per-chunk LDS (child fronts) small.
   static constexpr int NM = NJ * M;
   static constexpr int BP2 = NM <= 100 ? 64 :(NM <= 200 ? 16 : (NM <= 1000 ? 8 : 2));
-  static constexpr int BP = LBK >= 2 ? BP2 : BP1;  // LBK 3 = LB2 with packed LDS records
+  static constexpr int BP = LBK >= 2 ? BP2 : BP1;  // LBK 5 = LB2 with packed two-child walks
   // 50-job LB2 (NM 500..1000): 8-parent chunks, half as many per iteration (same
   // 16K-parent window, half the per-chunk barriers; the smaller chunk-count prefix
   // pays for the larger child arrays in LDS)
@@ -91,9 +91,7 @@ struct PfspArgs {
   int sum_all[M];
   uint8_t pm0[PfspConsts<M>::P];
   uint8_t pm1[PfspConsts<M>::P];
-  // LB2 expand variants (A/B knobs, both off by default; after the tables so the
-  // LB1 kernels' argument layout is unchanged)
-  int lb2_wave;            // wave-uniform pair walks (1) or dense (pair, child) tasks (0)
+  // LB2 expand knob (after the tables so the LB1 kernels' argument layout is unchanged)
   int lb2_rounds;          // B2 in rounds of pairs, re-compacting the children still below best
   // element-wise probe of the expand kernel (tests): bound of every child of window
   // parent i at dbg_lb[dbg_off[i] + (k - depth)] (exact LB2 below best, else >= best)
@@ -105,10 +103,6 @@ struct PfspArgs {
   const uint4* recs4;
   int rs4;
   int lb2_pipe;
-  // LB2 chunks dealt dynamically (a per-iteration counter in the control slot) instead
-  // of chunk = blockIdx.x + k * gridDim.x: active children per chunk vary ~4x, and a
-  // static deal leaves the iteration waiting on its unluckiest workgroup
-  int lb2_dyn;
   // LB2 chunk ch takes window parents ch, ch + nchunks, ch + 2 nchunks, ... instead of
   // BP consecutive ones: consecutive pool nodes are siblings with similar work, so
   // consecutive chunks ranged from 0 to ~4x the mean active children and the slowest
@@ -482,7 +476,7 @@ __device__ inline void pfsp_lb1_parent(const PfspArgs<NJ, M>& a, Smem& sm, int p
 template <int NJ, int M>
 __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t);
 
-template <int NJ, int M, bool PACK, bool PS, bool PK = false>
+template <int NJ, int M, bool PK = false>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 
 // Occupancy: the LB1 kernels are latency-bound (profiles/r1/r1o), so the register
@@ -490,19 +484,18 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t);
 // spills); LB2 is bounded by its LDS footprint instead (4 workgroups per CU for
 // 50 x 20), and the packed-walk kernel (LBK 5) is held to the 128 VGPRs of 4 waves
 // per SIMD (its unrolled walk would otherwise take 130).
+// (Variants measured slower and removed in round 3, numbers in profiles/r2/lb2_variants.md
+// and profiles/r1/r1af: every record packed in LDS, prefix/suffix walks per (parent,
+// pair), wave-uniform pair walks, a dynamic chunk queue.)
 template <int NJ, int M, int LBK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK == 5 ? 4 : LBK >= 2 ? 1 : (M <= 10 ? 6 : 4))))
 void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
-    pfsp_expand_lb2<NJ, M, false, false>(a, t);
-  else if constexpr (LBK == 3)
-    pfsp_expand_lb2<NJ, M, true, false>(a, t);  // records packed in LDS
-  else if constexpr (LBK == 4)
-    pfsp_expand_lb2<NJ, M, false, true>(a, t);  // prefix/suffix walks per (parent, pair)
+    pfsp_expand_lb2<NJ, M>(a, t);
   else if constexpr (LBK == 5 && NJ <= 64)
-    pfsp_expand_lb2<NJ, M, false, false, true>(a, t);  // two children per lane, packed u16 walks
+    pfsp_expand_lb2<NJ, M, true>(a, t);  // two children per lane, packed u16 walks
   else if constexpr (LBK == 5)
-    pfsp_expand_lb2<NJ, M, false, false>(a, t);  // (job sets of one word only)
+    pfsp_expand_lb2<NJ, M>(a, t);  // (job sets of one word only)
   else
     pfsp_expand_lb1<NJ, M>(a, t);  // permutation nodes (20-job instances use pfsp_front_kernels.hpp)
 }
@@ -522,15 +515,13 @@ void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
 //       is skipped (the reference's early exit, c_bound_johnson.c:231-234: only
 //       the lb < best decision matters, and it is unchanged).
 //   B3  survivors (LB2 < best) -> ballot bitmap -> compaction as in every kernel.
-template <int NJ, int M, bool PACK = false>
+template <int NJ, int M>
 struct PfspSmemLB2 {
   using G = PfspGeom<NJ, 2, M>;
   using C = PfspConsts<M>;
-  // PACK (kernel LBK 3): every pair's records in LDS, 4 B each {job:6 | p0:7 | p1:7 |
-  // lag:12}, in evaluation order (50 x 20: 38 KB)
   // records in LDS when they fit 32 KB (20 x 20: 30 KB); otherwise (50 x 20: 76 KB)
   // they are read from L2 (packing the leading pairs to 4 B in LDS measured no gain,
-  // profiles/r1/r1ag)
+  // profiles/r1/r1ag; all of them in LDS halved the occupancy, profiles/r2/lb2_variants.md)
   static constexpr bool kRecsInLds = C::P * NJ * 8 <= 32 * 1024;
   PfspNode<NJ> node[G::BP];
   uint32_t fr[G::BP][M];                  // parent front | remain << 16
@@ -543,239 +534,29 @@ struct PfspSmemLB2 {
   int lbv[G::MAXCH];                      // active child LB2 (max over pairs)
   int16_t act[G::MAXCH];                  // child -> active slot, -1 if decided in B1
   int16_t alist[G::MAXCH];                // B2 rounds: active slots still below best
-  int16_t jslot[G::BP][NJ];               // B2 prefix/suffix: (parent, job) -> active slot or -1
   uint8_t aparent[G::MAXCH];              // active slot -> chunk parent
   uint8_t ajob[G::MAXCH];                 // active slot -> its job
-  u64 amask[G::BP];                       // jobs of the parent's children still below best (NJ <= 64)
-  uint8_t palive[G::BP];                  // parent still has an active child below best
-  uint8_t plist[G::BP];                   // ... compacted
-  int npl;
-  int qch;                                // next chunk (dynamic deal)
   u64 bits[G::NWORDS + kBlock / kWave];
   int wpre[kBlock];
   int scan[kBlock / kWave];
   int red[kBlock / kWave];
   uint2 pinfo[C::P];
   uint2 recs[kRecsInLds ? C::P * NJ : 1];
-  uint32_t rpk[PACK ? C::P * NJ : 1];
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
-// B2, wave-uniform variant: a wave walks ONE machine pair for up to 64 active
-// children (lane = child). The pair's Johnson records are then the same for every
-// lane, so they are read with scalar loads (constant address space: the tables are
-// written once, before the engine's first launch) into SGPRs and enter the VALU as
-// scalar operands. The dense variant above spends a per-lane 8-B load (L2 latency:
-// the 50x20 tables are 76 KB, larger than L1) plus its unpacking on every step.
-// Cost: lanes past the active count idle (a chunk's active list is rarely a whole
-// number of waves). profiles/r1/r1ae (dense: 60 % of wave cycles waiting); measured
-// 2.6x slower on ta056 (profiles/r1/r1af: active children per chunk fill a fraction of
-// a wave), so it is off by default (TTS_LB2_WAVE=1 turns it on).
+// Records read with scalar loads (constant address space: the tables are written
+// once, before the engine's first launch) when every active lane walks the same pair.
 using kconst_u64 = const __attribute__((address_space(4))) unsigned long long;  // {x, y} of a uint2
 
+// One Johnson walk (ref c_bound_johnson.c:190-209) of machine pair `pi` from child
+// fronts (t0, t1) over the jobs not in `msk`. Records come from `recs` (LDS or L2),
+// or with scalar loads when every lane of the wave walks the same pair (uniform_ref).
 template <int NJ, int M, class S>
-__device__ inline void lb2_walks_wave(const PfspArgs<NJ, M>& a, S& sm, int nact, int best) {
+__device__ inline void lb2_johnson_walk(const uint2* recs, uint2 pi, int N, const u64 (&msk)[PfspGeom<NJ, 2, M>::NW],
+                                        int& t0, int& t1, int uniform_ref = -1) {
   using G = PfspGeom<NJ, 2, M>;
-  const int P = a.npairs;
-  constexpr int NWAVE = kBlock / kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-  kconst_u64* const pinfo = (kconst_u64*)(uintptr_t)a.pinfo;
-  kconst_u64* const recs = (kconst_u64*)(uintptr_t)a.recs;
-  const int N = a.jobs;
-  for (int base = 0; base < nact; base += kWave) {
-    const int ai = base + lane;
-    const int aic = ai < nact ? ai : nact - 1;
-    for (int q = wave; q < P; q += NWAVE) {
-      const bool on = ai < nact && sm.lbv[aic] < best;
-      if (__ballot(on) == 0) continue;
-      const u64 piw = pinfo[q];
-      const uint2 pi = make_uint2(static_cast<uint32_t>(piw), static_cast<uint32_t>(piw >> 32));
-      int t0 = sm.cf[pi.x & 0xff][aic], t1 = sm.cf[(pi.x >> 8) & 0xff][aic];
-      u64 msk[G::NW];
-#pragma unroll
-      for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[aic][w];
-      kconst_u64* const rq = recs + static_cast<int>(pi.x >> 16) * N;
-#pragma unroll 8
-      for (int r = 0; r < N; ++r) {
-        const u64 rw = rq[r];
-        const uint32_t rx = static_cast<uint32_t>(rw), ry = static_cast<uint32_t>(rw >> 32);
-        const int n0 = t0 + static_cast<int>(rx >> 16);
-        const int n1 = max(t1, n0 + static_cast<int>(ry >> 16)) + static_cast<int>(ry & 0xffff);
-        const bool sched = job_in<G::NW>(msk, static_cast<int>(rx & 0xffff));
-        t0 = sched ? t0 : n0;
-        t1 = sched ? t1 : n1;
-      }
-      if (on) atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
-    }
-  }
-}
-
-// B2, prefix/suffix form (default). For one machine pair (m0, m1) the Johnson walk
-// of a child (ref c_bound_johnson.c:190-209: t0 += p0, t1 = max(t1, t0 + lag) + p1
-// over the unscheduled jobs in Johnson order) unrolls, in max-plus algebra, to
-//     t1 = max( T1 + S1', T0 + max_j (A'_j + lag_j + B'_j) )
-// with T0/T1 the child's front on m0/m1, A'_j the p0 prefix up to j and B'_j the p1
-// suffix from j over the child's unscheduled set U' = U \ {c}, S1' = sum of p1 over
-// U'. Relative to the PARENT's set U (w_j = A_j - Pb_j + lag_j, Pb_j the p1 prefix
-// before j, S1 = sum of p1 over U), removing c lowers every later A by p0_c and
-// every earlier B by p1_c, so for child c:
-//     T0 + max_j(...) = T0 + S1 + max( max_{j<c} w_j - p1_c , max_{j>c} w_j - p0_c ).
-// One forward walk per (parent, pair) gives every child its prefix term, one
-// backward walk its suffix term: O(N) per (parent, pair) instead of O(N) per
-// (child, pair). The remaining terms of the pair bound, T1 + S1' + tail1 and
-// t0 + tail0, are LB1 machine terms, so lbv starts at LB1 and both walks only raise
-// it (LDS max). The value is the exact LB2 (all pairs, no early exit); a parent
-// leaves the task list once all its children exceed best (rounds of pairs in the
-// learned early-exit order), which changes no prune decision.
-template <int NJ, int M, bool PACK, class S>
-__device__ inline void lb2_ps_walks(const PfspArgs<NJ, M>& a, S& sm, int nvalid, int nact, int best) {
-  using G = PfspGeom<NJ, 2, M>;
-  const int P = a.npairs;
-  static_assert(G::BP <= kWave, "parent list is built by one wave");
-  constexpr bool kReg = NJ <= 64;  // one pass, the walk's w values in registers
-  const int tid = threadIdx.x;
-  const int N = a.jobs;
-  const uint2* recs = S::kRecsInLds ? sm.recs : a.recs;
-  auto build_plist = [&]() {
-    if (tid < G::BP) {
-      sm.palive[tid] = 0;
-      sm.amask[tid] = 0;
-    }
-    __syncthreads();
-    for (int s = tid; s < nact; s += kBlock)
-      if (sm.lbv[s] < best) {
-        sm.palive[sm.aparent[s]] = 1;
-        if constexpr (kReg) atomicOr(&sm.amask[sm.aparent[s]], 1ull << sm.ajob[s]);
-      }
-    __syncthreads();
-    if (tid < kWave) {
-      const bool al = tid < nvalid && sm.palive[tid];
-      const u64 b = __ballot(al);
-      if (al) sm.plist[__popcll(b & lanemask_lt())] = static_cast<uint8_t>(tid);
-      if (tid == 0) sm.npl = __popcll(b);
-    }
-    __syncthreads();
-  };
-  // record r of pair slot qs: {job, p0, p1, lag}
-  auto rec = [&](int qs, uint2 pi, int r, int& j, int& p0, int& p1, int& lag) {
-    if constexpr (PACK) {
-      const uint32_t w = sm.rpk[qs * N + r];
-      j = static_cast<int>(w & 63u);
-      p0 = static_cast<int>((w >> 6) & 127u);
-      p1 = static_cast<int>((w >> 13) & 127u);
-      lag = static_cast<int>(w >> 20);
-    } else {
-      const uint2 rc = recs[static_cast<int>(pi.x >> 16) * N + r];
-      j = static_cast<int>(rc.x & 0xffff);
-      p0 = static_cast<int>(rc.x >> 16);
-      p1 = static_cast<int>(rc.y & 0xffff);
-      lag = static_cast<int>(rc.y >> 16);
-    }
-  };
-  build_plist();
-  int q0 = 0, R = 8;
-  while (q0 < P) {
-    const int np = sm.npl;
-    if (np == 0) break;
-    const int nq = min(P - q0, max(R, (kBlock + np - 1) / np));
-    const int ntask = np * nq;
-    for (int task = tid; task < ntask; task += kBlock) {
-      const int qq = task / np;
-      const int p = sm.plist[task - qq * np];
-      const int qs = q0 + qq;
-      const uint2 pi = sm.pinfo[qs];
-      const int m0 = pi.x & 0xff, m1 = (pi.x >> 8) & 0xff;
-      const int tail1 = static_cast<int>(pi.y >> 16);
-      const int S0 = static_cast<int>(sm.fr[p][m0] >> 16), S1 = static_cast<int>(sm.fr[p][m1] >> 16);
-      const int K = S1 + tail1;
-      u64 msk[G::NW];
-#pragma unroll
-      for (int w = 0; w < G::NW; ++w) msk[w] = sm.pmask[p][w];
-      const int16_t* js = sm.jslot[p];
-      const uint16_t* c0 = sm.cf[m0];
-      if constexpr (kReg) {
-        // forward: prefix terms at the live children, w_j kept per position
-        const u64 am = sm.amask[p];
-        int wv[NJ];
-        u64 um = 0, cm = 0;  // positions in U / positions of live children
-        int A = 0, Pb = 0, pre = INT_MIN / 4;
-#pragma unroll
-        for (int r = 0; r < NJ; ++r) {
-          wv[r] = 0;
-          if (r < N) {
-            int j, p0, p1, lag;
-            rec(qs, pi, r, j, p0, p1, lag);
-            if (!((msk[0] >> j) & 1ull)) {
-              A += p0;
-              if ((am >> j) & 1ull) {
-                const int sl = js[j];
-                atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p1 + pre);
-                cm |= 1ull << r;
-              }
-              wv[r] = A - Pb + lag;
-              pre = max(pre, wv[r]);
-              Pb += p1;
-              um |= 1ull << r;
-            }
-          }
-        }
-        // backward over the kept values: suffix terms (records re-read only at live children)
-        int suf = INT_MIN / 4;
-#pragma unroll
-        for (int r = NJ - 1; r >= 0; --r) {
-          if ((cm >> r) & 1ull) {
-            int j, p0, p1, lag;
-            rec(qs, pi, r, j, p0, p1, lag);
-            const int sl = js[j];
-            atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p0 + suf);
-          }
-          if ((um >> r) & 1ull) suf = max(suf, wv[r]);
-        }
-      } else {
-        // forward: prefix maxima
-        int A = 0, Pb = 0, pre = INT_MIN / 4;
-        for (int r = 0; r < N; ++r) {
-          int j, p0, p1, lag;
-          rec(qs, pi, r, j, p0, p1, lag);
-          if (job_in<G::NW>(msk, j)) continue;
-          A += p0;
-          const int sl = js[j];
-          if (sl >= 0) atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p1 + pre);
-          pre = max(pre, A - Pb + lag);
-          Pb += p1;
-        }
-        // backward: suffix maxima (A_j = S0 - p0 after j, Pb_j = S1 - p1 from j on)
-        int SA = 0, SB = 0, suf = INT_MIN / 4;
-        for (int r = N - 1; r >= 0; --r) {
-          int j, p0, p1, lag;
-          rec(qs, pi, r, j, p0, p1, lag);
-          if (job_in<G::NW>(msk, j)) continue;
-          const int sl = js[j];
-          if (sl >= 0) atomicMax(&sm.lbv[sl], static_cast<int>(c0[sl]) + K - p0 + suf);
-          SB += p1;
-          suf = max(suf, (S0 - SA) - (S1 - SB) + lag);
-          SA += p0;
-        }
-      }
-    }
-    q0 += nq;
-    R *= 2;
-    __syncthreads();  // this round's maxima are final
-    if (q0 >= P) break;
-    build_plist();
-  }
-}
-
-// One Johnson walk (ref c_bound_johnson.c:190-209) of machine pair slot `qs` (pair
-// info `pi`) from child fronts (t0, t1) over the jobs not in `msk`. Records come from
-// LDS (packed 4 B, PACK) or from `recs` (LDS or L2).
-template <int NJ, int M, bool PACK, class S>
-__device__ inline void lb2_johnson_walk(const S& sm, const uint2* recs, int qs, uint2 pi, int N,
-                                        const u64 (&msk)[PfspGeom<NJ, 2, M>::NW], int& t0, int& t1,
-                                        int uniform_ref = -1) {
-  using G = PfspGeom<NJ, 2, M>;
-  if constexpr (!PACK && !S::kRecsInLds) {
+  if constexpr (!S::kRecsInLds) {
     // every active lane of the wave walks the same pair: the records are wave-uniform,
     // read with scalar loads (constant address space, scalar cache) into SGPRs instead
     // of one vector load per step (the tables are written before the first launch)
@@ -794,28 +575,15 @@ __device__ inline void lb2_johnson_walk(const S& sm, const uint2* recs, int qs, 
       return;
     }
   }
-  if constexpr (PACK) {
-    const uint32_t* rq = sm.rpk + qs * N;
+  const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
 #pragma unroll 4
-    for (int r = 0; r < N; ++r) {
-      const uint32_t w = rq[r];
-      const int n0 = t0 + static_cast<int>((w >> 6) & 127u);
-      const int n1 = max(t1, n0 + static_cast<int>(w >> 20)) + static_cast<int>((w >> 13) & 127u);
-      const bool sched = job_in<G::NW>(msk, static_cast<int>(w & 63u));
-      t0 = sched ? t0 : n0;
-      t1 = sched ? t1 : n1;
-    }
-  } else {
-    const uint2* rq = recs + static_cast<int>(pi.x >> 16) * N;
-#pragma unroll 4
-    for (int r = 0; r < N; ++r) {
-      const uint2 rc = rq[r];
-      const int n0 = t0 + static_cast<int>(rc.x >> 16);
-      const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
-      const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
-      t0 = sched ? t0 : n0;
-      t1 = sched ? t1 : n1;
-    }
+  for (int r = 0; r < N; ++r) {
+    const uint2 rc = rq[r];
+    const int n0 = t0 + static_cast<int>(rc.x >> 16);
+    const int n1 = max(t1, n0 + static_cast<int>(rc.y >> 16)) + static_cast<int>(rc.y & 0xffff);
+    const bool sched = job_in<G::NW>(msk, static_cast<int>(rc.x & 0xffff));
+    t0 = sched ? t0 : n0;
+    t1 = sched ? t1 : n1;
   }
 }
 
@@ -906,11 +674,11 @@ __device__ inline void lb2_walk_pipe2(const uint4* rq, int ndouble, u64 ma, u64 
   }
 }
 
-template <int NJ, int M, bool PACK, bool PS, bool PK>
+template <int NJ, int M, bool PK>
 __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   using G = PfspGeom<NJ, 2, M>;
   using C = PfspConsts<M>;
-  using S = PfspSmemLB2<NJ, M, PACK>;
+  using S = PfspSmemLB2<NJ, M>;
   using Node = PfspNode<NJ>;
   constexpr int VPN = sizeof(Node) / 16;
   constexpr int NWD = sizeof(Node) / 4;
@@ -919,8 +687,6 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   const unsigned long long t_entry = a.dbg_blk ? wall_clock64() : 0;
-  // the next iteration's chunk queue (its slot is not read by this iteration)
-  if (a.lb2_dyn && blockIdx.x == 0 && tid == 0) pa.ctl->slot[(t + 1) % 3].qnext = 0;
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
   if (v.B == 0 || v.overflow) return;
   const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -934,33 +700,17 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     for (int i = tid; i < P; i += kBlock) sm.pinfo[i] = a.pinfo[i];
     if constexpr (S::kRecsInLds)
       for (int i = tid; i < P * a.jobs; i += kBlock) sm.recs[i] = a.recs[i];
-    if constexpr (PACK)
-      for (int i = tid; i < P * a.jobs; i += kBlock) {
-        const int slot = i / a.jobs, r = i - slot * a.jobs;
-        const uint2 rc = a.recs[static_cast<int>(a.pinfo[slot].x >> 16) * a.jobs + r];
-        sm.rpk[i] = (rc.x & 0xffffu) | ((rc.x >> 16) << 6) | ((rc.y & 0xffffu) << 13) | ((rc.y >> 16) << 20);
-      }
   }
   const uint2* recs = S::kRecsInLds ? sm.recs : a.recs;
   const int N = a.jobs;
-  const bool pipe = !PACK && !S::kRecsInLds && a.lb2_pipe;
+  const bool pipe = !S::kRecsInLds && a.lb2_pipe;
   const int ndouble = (N + 7) >> 3;
   unsigned long long tm[4] = {0, 0, 0, 0}, tc = 0;
   const bool timed = a.dbg_time != nullptr;
-  const bool dyn = a.lb2_dyn != 0;
   const bool stride = a.lb2_stride != 0;
-  int* const qctr = &pa.ctl->slot[t % 3].qnext;
-  int ch = blockIdx.x;
-  if (dyn) {
-    if (tid == 0) sm.qch = atomicAdd(qctr, 1);
-    __syncthreads();
-    ch = sm.qch;
-  }
   int nchunks_done = 0;
   const unsigned long long t_pro = a.dbg_blk ? wall_clock64() : 0;
-  while (ch < v.nchunks) {
-    int qn = 0;
-    if (dyn && tid == 0) qn = atomicAdd(qctr, 1);  // next chunk, requested a chunk ahead
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     ++nchunks_done;
     if (timed) tc = clock64();
     // window parents of this chunk: ch + i * nchunks (strided) or ch * BP + i
@@ -989,7 +739,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     int my_leaves = 0, nact = 0;
     for (int cb = 0; cb < total; cb += kBlock) {
       const int c = cb + tid;
-      int active = 0, job = 0, p = 0, lb1c = 0;
+      int active = 0, job = 0, p = 0;
       int f[M];
       if (c < total) {
         p = sm.map[c];
@@ -1018,14 +768,12 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         } else {
           active = (keep && lb1 < best) ? 1 : 0;
         }
-        lb1c = lb1;
         if (a.dbg_lb && !active) a.dbg_lb[a.dbg_off[gidx(p)] + (k - d)] = lb1;
       }
       int cnt = 0;
       const int slot = nact + block_exclusive_scan(active, sm.scan, &cnt);
       if (c < total) {
         sm.act[c] = static_cast<int16_t>(active ? slot : -1);
-        sm.jslot[p][job] = static_cast<int16_t>(active ? slot : -1);
       }
       if (active) {
 #pragma unroll
@@ -1033,7 +781,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
 #pragma unroll
         for (int w = 0; w < G::NW; ++w)
           sm.cm[slot][w] = sm.pmask[p][w] | (((job >> 6) == w) ? (1ull << (job & 63)) : 0ull);
-        sm.lbv[slot] = PS ? lb1c : 0;
+        sm.lbv[slot] = 0;
         sm.aparent[slot] = static_cast<uint8_t>(p);
         sm.ajob[slot] = static_cast<uint8_t>(job);
       }
@@ -1046,11 +794,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       tc = c;
     }
     // ---- B2: (pair, child) Johnson walks, pair-major ----
-    if constexpr (PS) {
-      if (nact > 0) lb2_ps_walks<NJ, M, PACK>(a, sm, nvalid, nact, best);
-    } else if (nact > 0 && a.lb2_wave) {
-      lb2_walks_wave<NJ, M>(a, sm, __builtin_amdgcn_readfirstlane(nact), best);
-    } else if (nact > 0 && a.lb2_rounds) {
+    if (nact > 0 && a.lb2_rounds) {
       // Rounds of 8, 16, 32, ... pairs (learned early-exit order: the first pairs
       // prune most children). Between rounds the children whose LB2 already exceeds
       // best are dropped from the task list, so a wave's lanes no longer idle on
@@ -1111,7 +855,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
             if (pipe && uref < 0)
               lb2_walk_pipe<G::NW>(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, msk, t0, t1);
             else
-              lb2_johnson_walk<NJ, M, PACK>(sm, recs, q0 + qq, pi, N, msk, t0, t1, uref);
+              lb2_johnson_walk<NJ, M, S>(recs, pi, N, msk, t0, t1, uref);
             atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
           }
           ii += di;
@@ -1158,7 +902,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
           u64 msk[G::NW];
 #pragma unroll
           for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
-          lb2_johnson_walk<NJ, M, PACK>(sm, recs, q, pi, N, msk, t0, t1, uref);
+          lb2_johnson_walk<NJ, M, S>(recs, pi, N, msk, t0, t1, uref);
           atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
         }
         ai += da;
@@ -1223,13 +967,6 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
     }
     __syncthreads();
     if (timed) tm[3] += clock64() - tc;
-    if (dyn) {
-      if (tid == 0) sm.qch = qn;
-      __syncthreads();
-      ch = sm.qch;
-    } else {
-      ch += gridDim.x;
-    }
   }
   if (timed && tid == 0) {
     const unsigned long long tot = tm[0] + tm[1] + tm[2] + tm[3];

@@ -36,7 +36,6 @@ struct PoolCtl {
     u64 stack;  // ring occupancy at the start of iteration t
     int nch;    // chunks written by iteration t-1 into buffer t%2
     int sdone;  // armed rank split already done (see split_world)
-    int qnext;  // chunk queue of kernels that deal chunks dynamically (LB2); reset by iteration t-1
   };
   Slot slot[3];
   // plain counters, updated by workgroup 0 (or the host between launches)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Parameterised GPU-box session: scripts/gpu_run.sh <out-dir> <step>...
-# steps: tests[:<pytest -k expr>] | bench1 | bench2shared | smoke | lb2:<ta056 seconds>[@ENV=V,...] | trace:<workload>
+# steps: tests[:<k1>,<k2>...] (pytest -k "k1 or k2") | bench1 | bench2shared | smoke | lb2:<ta056 seconds>[@ENV=V,...] | trace:<workload>
 # Every step runs under its own timeout; the session stops at the first failure.
 set -o pipefail
 out=gpurun_out/$1; shift
@@ -8,7 +8,7 @@ mkdir -p "$out"
 for step in "$@"; do
   case "$step" in
     tests*)
-      k="${step#tests}"; k="${k#:}"
+      k="${step#tests}"; k="${k#:}"; k="${k//,/ or }"   # tests:a,b -> -k "a or b"
       echo "[gpu_run] pytest -m gpu ${k:+-k $k}"
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${k:+-k "$k"} \
         > "$out/gpu_tests.log" 2>&1 || { tail -30 "$out/gpu_tests.log"; exit 1; }

@@ -19,10 +19,9 @@ from dist_gpu_accelerated_tree_search_amd import PfspModel
 from dist_gpu_accelerated_tree_search_amd.ops import hip
 
 VARIANTS = [
-    ("plain walk, blocked chunks", 1, {"TTS_LB2_PIPE": "0", "TTS_LB2_DYN": "0", "TTS_LB2_STRIDE": "0"}),
-    ("packed 2-child, blocked", 4, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "0", "TTS_LB2_STRIDE": "0"}),
-    ("packed 2-child, strided", 4, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "0", "TTS_LB2_STRIDE": "1"}),
-    ("packed 2-child, strided, dyn", 4, {"TTS_LB2_PIPE": "1", "TTS_LB2_DYN": "1", "TTS_LB2_STRIDE": "1"}),
+    ("plain walk, blocked chunks", 1, {"TTS_LB2_PIPE": "0", "TTS_LB2_STRIDE": "0"}),
+    ("packed 2-child, blocked", 4, {"TTS_LB2_PIPE": "1", "TTS_LB2_STRIDE": "0"}),
+    ("packed 2-child, strided", 4, {"TTS_LB2_PIPE": "1", "TTS_LB2_STRIDE": "1"}),
 ]
 
 

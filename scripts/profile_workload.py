@@ -66,6 +66,25 @@ elif which.startswith("spill021"):  # spill021[:ring_MB[:seconds]]: ta021 LB1_d,
           f"{dt:.2f} s, spilled {st['spilled']} refilled {st['refilled']} pinned MB {st['pinned_bytes'] >> 20} "
           f"pool device {st['device_nodes']} host {st['host_nodes']}")
     raise SystemExit(0)
+elif which.startswith("spillbig"):  # spillbig[:seconds]: ta021 LB1_d begun from a 2M-node host frontier on a
+    # 1024-parent window and the smallest ring it allows (~10 MB): the frontier spills to pinned host
+    # blocks at begin() and comes back through refills while graph replays run
+    import time
+    parts = which.split(":")
+    box = float(parts[1]) if len(parts) > 1 else 3.0
+    ring = int(parts[2]) << 20 if len(parts) > 2 else 1 << 20
+    m = PfspModel(21, 0)
+    nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 2_000_000)
+    eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=ring))
+    t0 = time.perf_counter()
+    eng.begin(nodes, int(best))
+    eng.run(max_seconds=box)
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    print(which, f"{len(nodes)} begin nodes, capacity {st['capacity']} nodes: {st['tree'] / dt / 1e9:.3f} G nodes/s "
+          f"over {dt:.2f} s, spilled {st['spilled']} refilled {st['refilled']} pinned MB {st['pinned_bytes'] >> 20} "
+          f"pool device {st['device_nodes']} host {st['host_nodes']}")
+    raise SystemExit(0)
 elif which == "queens":
     m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=32 << 30))
     r = solve_engine(m, eng)

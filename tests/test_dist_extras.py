@@ -124,11 +124,12 @@ def test_cpu_worker_per_rank(world, problem, tmp_path):
     # -C 1 in the process-per-rank runtime: every rank's engine is a hybrid of its main
     # engine and a CPU worker thread (csrc/core/hybrid_engine.hpp); golden tree, and the
     # CPU workers explore part of it (two workers per rank in the statistics)
-    spec = {"problem": problem, "inst": 14, "lb": 1, "N": 11, "backend": "cpu", "session": True, "repeat": 2,
+    # N=12: a tree large enough that each rank's CPU worker is handed work even on a loaded host
+    spec = {"problem": problem, "inst": 14, "lb": 1, "N": 12, "backend": "cpu", "session": True, "repeat": 2,
             "engine": {"cpu_batch": 64},
             "dist": {"cpu_workers": 2, "cpu_batch": 64, "m": 8, "init_per_rank": 16}}
     res = spawn_local(world, solve_rank, (spec,), timeout=300)
-    gold = GOLD if problem == "pfsp" else (166925, 2680, None)
+    gold = GOLD if problem == "pfsp" else (856188, 14200, None)
     for r in res:
         assert (r["tree"], r["sol"]) == gold[:2]
     ws = res[0]["workers"]

@@ -20,12 +20,11 @@ def test_pfsp_golden_on_gpu(key):
     assert (r.tree, r.sol, r.best) == GOLDEN[key]
 
 
-@pytest.mark.parametrize("ps,rounds,pk", [("1", "1", "0"), ("0", "0", "0"), ("0", "1", "0"), ("0", "1", "1")])
-def test_lb2_pair_rounds_golden(ps, rounds, pk, monkeypatch):
+@pytest.mark.parametrize("rounds,pk", [("0", "0"), ("1", "0"), ("1", "1")])
+def test_lb2_pair_rounds_golden(rounds, pk, monkeypatch):
     # every B2 schedule on 20x10 LB2 trees (20x5: ta010 in the test below): the
-    # prefix/suffix walks, the per-child walks with/without rounds, and the rounds of
-    # packed two-child walks (the default)
-    monkeypatch.setenv("TTS_LB2_PS", ps)
+    # per-child walks with/without rounds, and the rounds of packed two-child walks
+    # (the default)
     monkeypatch.setenv("TTS_LB2_ROUNDS", rounds)
     monkeypatch.setenv("TTS_LB2_PK", pk)
     for key in ((14, 2), (16, 2)):
@@ -49,18 +48,15 @@ def test_pfsp_bigger_trees_on_gpu():
 TA056_TIGHT = {140: (78361, 0, 3539), 135: (454770, 0, 3544)}
 
 
-@pytest.mark.parametrize("ps,wave,rounds,pk", [("1", "0", "1", "0"), ("0", "0", "1", "0"), ("0", "0", "0", "0"),
-                                               ("0", "1", "0", "0"), ("0", "0", "1", "1")])
-def test_ta056_lb2_tight_incumbent(ps, wave, rounds, pk, monkeypatch):
-    monkeypatch.setenv("TTS_LB2_PS", ps)  # prefix/suffix walks per (parent, pair)
-    monkeypatch.setenv("TTS_LB2_WAVE", wave)  # wave-uniform pair walks / dense (pair, child) tasks
+@pytest.mark.parametrize("rounds,pk", [("1", "0"), ("0", "0"), ("1", "1")])
+def test_ta056_lb2_tight_incumbent(rounds, pk, monkeypatch):
     monkeypatch.setenv("TTS_LB2_ROUNDS", rounds)  # pair rounds with re-compacted children
     monkeypatch.setenv("TTS_LB2_PK", pk)  # rounds of packed two-child walks (default)
     model = PfspModel(56, 2)
     eng = model.make_engine("gpu", 0, SMALL)
     for gap, gold in TA056_TIGHT.items():
         r = solve_engine(model, eng, best=model.best_known - gap)
-        assert (r.tree, r.sol, r.best) == gold, (wave, gap)
+        assert (r.tree, r.sol, r.best) == gold, (rounds, pk, gap)
 
 
 @pytest.mark.parametrize("N,gold", [(8, (2056, 92)), (12, (856188, 14200)), (14, (27358552, 365596)),
