@@ -116,6 +116,20 @@ inline void bind_engine(py::module_& m) {
       .def_property("best", &IEngine::best, &IEngine::set_best)
       .def("reset_counters", &IEngine::reset_counters)
       .def("stats", [](IEngine& e) { return engine_stats_dict(e.stats()); })
+      .def("set_trace", &IEngine::set_trace, py::arg("on"))
+      .def(
+          "trace",
+          [](IEngine& e) {
+            std::vector<double> v;
+            {
+              py::gil_scoped_release nogil;
+              v = e.trace();
+            }
+            py::array_t<double> a({static_cast<py::ssize_t>(v.size() / 3), static_cast<py::ssize_t>(3)});
+            std::copy(v.begin(), v.end(), a.mutable_data());
+            return a;
+          },
+          "(n, 3) array of {kind, start ms, end ms}: 0 graph replay, 1 spill D2H, 2 refill H2D")
       .def("synchronize", &IEngine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("transfer_stream", &IEngine::transfer_stream,
                              "Stream on which work-sharing sends/receives are enqueued (0: host engine).")

@@ -87,6 +87,13 @@ class IEngine {
   // of the search space below a node of depth d, 1 - pool_weight is the explored
   // fraction of the space (the B&B progress measure of tools/progress estimates).
   virtual double pool_weight(const std::vector<double>& w) { (void)w; return 0; }
+  // Device timeline of graph replays and pool copies (GPU engines; evidence that the
+  // pinned spill/refill overlaps the search): set_trace(true) starts a fresh record,
+  // trace() returns {kind, start ms, end ms} triples relative to the first record,
+  // kind 0 = graph replay (compute stream), 1 = spill D2H, 2 = refill H2D (transfer
+  // stream). Timing events around each launch; off by default.
+  virtual void set_trace(bool on) { (void)on; }
+  virtual std::vector<double> trace() { return {}; }
   virtual size_t size() = 0;
   // Replays expand graphs until the pool is empty, `max_launches` graphs were
   // launched (<0: unlimited), `max_seconds` elapsed (<=0: unlimited), or the pool

@@ -163,6 +163,7 @@ class DeviceEngine final : public IEngine {
     (void)hipSetDevice(cfg_.device);
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (xfer_) (void)hipStreamSynchronize(xfer_);
+    trace_clear();
     spill_.clear();
     for (auto& gp : graphs_)
       for (auto& gs : gp)
@@ -195,6 +196,27 @@ class DeviceEngine final : public IEngine {
   uintptr_t stream() const override { return reinterpret_cast<uintptr_t>(stream_); }
   uintptr_t transfer_stream() const override { return reinterpret_cast<uintptr_t>(xfer_); }
   void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
+  void set_trace(bool on) override {
+    trace_clear();
+    trace_ = on;
+  }
+  std::vector<double> trace() override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    TTS_HIP_CHECK(hipStreamSynchronize(stream_));
+    TTS_HIP_CHECK(hipStreamSynchronize(xfer_));
+    std::vector<double> out;
+    if (trace_rec_.empty()) return out;
+    const hipEvent_t ref = trace_rec_.front().a;
+    for (const auto& r : trace_rec_) {
+      float a = 0, b = 0;
+      TTS_HIP_CHECK(hipEventElapsedTime(&a, ref, r.a));
+      TTS_HIP_CHECK(hipEventElapsedTime(&b, ref, r.b));
+      out.push_back(r.kind);
+      out.push_back(a);
+      out.push_back(b);
+    }
+    return out;
+  }
   void record_event(uintptr_t ev) override {
     if (!ev) return;
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
@@ -790,8 +812,10 @@ class DeviceEngine final : public IEngine {
       resv_.emplace_back(ev, k);
       reserved_ += k;
     };
+    const hipEvent_t tr = trace_ ? trace_mark(xfer_) : nullptr;
     spill_.push_from_device(d_ring_ + start, first, xfer_, reserve);
     if (first < n) spill_.push_from_device(d_ring_, n - first, xfer_, reserve);
+    if (tr) trace_rec_.push_back({1, tr, trace_mark(xfer_)});
     h_ctl_->bot = (h_ctl_->bot + n) & (cap_ - 1);
     h_ctl_->slot[0].stack -= n;
     stats_.spilled += n;
@@ -812,8 +836,10 @@ class DeviceEngine final : public IEngine {
     const size_t start = h_ctl_->bot & (cap_ - 1);
     const size_t first = std::min(n, cap_ - start);
     auto reserve = [&](hipEvent_t ev, size_t k) { ahead_.emplace_back(ev, k); };
+    const hipEvent_t tr = trace_ ? trace_mark(xfer_) : nullptr;
     spill_.push_from_device(d_ring_ + start, first, xfer_, reserve);
     if (first < n) spill_.push_from_device(d_ring_, n - first, xfer_, reserve);
+    if (tr) trace_rec_.push_back({1, tr, trace_mark(xfer_)});
     ahead_n_ = n;
   }
   void commit_spill_ahead() {
@@ -846,7 +872,9 @@ class DeviceEngine final : public IEngine {
     const size_t k = std::min({want, spill_.top_count(), limit - used, b0 ? b0 : cap_});
     if (k == 0) return false;
     Node* dst = d_ring_ + ((b0 + cap_ - k) & (cap_ - 1));
+    const hipEvent_t tr = trace_ ? trace_mark(xfer_) : nullptr;
     if (spill_.pop_to_device(dst, k, xfer_, &refill_ev_) != k) throw std::logic_error("pinned spill: short refill");
+    if (tr) trace_rec_.push_back({2, tr, trace_mark(xfer_)});
     refill_n_ = k;
     reserved_ += k;
     return true;
@@ -874,8 +902,10 @@ class DeviceEngine final : public IEngine {
     const int m = next_mirror_;
     next_mirror_ ^= 1;
     const int k = K > 0 ? K : ks_[gi];
+    const hipEvent_t tr = trace_ ? trace_mark(stream_) : nullptr;
     if (cfg_.use_graphs) {
       hipGraphExec_t g = K > 0 ? first_graph(K)[m] : graphs_[phase_ / 3][m][gi];
+      if (tr) TTS_HIP_CHECK(hipEventRecord(tr, stream_));  // after a first-use capture's sync
       TTS_HIP_CHECK(hipGraphLaunch(g, stream_));
     } else {
       for (int i = 0; i < k; ++i) Traits::launch(args_, (phase_ + i) % 6, grid_, stream_);
@@ -885,6 +915,7 @@ class DeviceEngine final : public IEngine {
       TTS_HIP_CHECK(hipGetLastError());
     }
     TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
+    if (tr) trace_rec_.push_back({0, tr, trace_mark(stream_)});
     push_inflight(m, k);
     phase_ = (phase_ + k) % 6;
     ++stats_.launches;
@@ -945,6 +976,30 @@ class DeviceEngine final : public IEngine {
   hipEvent_t up_done_ = nullptr;
   hipEvent_t ev_comp_ = nullptr, ev_xfer_ = nullptr;  // stream ordering (order())
   hipStream_t xfer_ = nullptr;                         // spills, refills, work-sharing sends/receives
+  // replay / copy timeline (set_trace): timing events, freed by trace_clear
+  struct TraceRec {
+    int kind;
+    hipEvent_t a, b;
+  };
+  std::vector<TraceRec> trace_rec_;
+  bool trace_ = false;
+  hipEvent_t trace_mark(hipStream_t s) {
+    hipEvent_t e = nullptr;
+    TTS_HIP_CHECK(hipEventCreate(&e));
+    TTS_HIP_CHECK(hipEventRecord(e, s));
+    return e;
+  }
+  void trace_clear() {
+    if (!trace_rec_.empty()) {
+      (void)hipStreamSynchronize(stream_);
+      (void)hipStreamSynchronize(xfer_);
+    }
+    for (auto& r : trace_rec_) {
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    trace_rec_.clear();
+  }
   std::deque<std::pair<hipEvent_t, size_t>> resv_;     // spill copies in flight (ring span reserved)
   size_t reserved_ = 0;                                // ring nodes reserved by copies in flight
   size_t refill_n_ = 0;                                // nodes of the refill in flight

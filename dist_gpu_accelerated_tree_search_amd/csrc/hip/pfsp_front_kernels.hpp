@@ -59,6 +59,9 @@ struct PfspFrontArgs {
   const int* offsets;
   int* bounds_out;
   int nparents;
+  // two-level iterations expand child-parallel (front_expand_cp, default) or one
+  // thread per parent (0, A/B runs: TTS_FUSED_CP=0)
+  int fused_cp;
 };
 
 template <int M>
@@ -67,6 +70,8 @@ struct FrontSmem {
   uint16_t ptab[G::NJ][G::MS];
   int scan[kBlock / kWave];
   uint4 mid[kBlock][G::VPN];  // level-1 survivors of a two-level chunk
+  uint4 par[G::BPF][G::VPN];  // a two-level chunk's parents (child-parallel expansion)
+  int coff[kBlock];           // child offsets of the nodes being expanded (child-parallel)
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -173,6 +178,159 @@ __device__ inline void front_emit(const FrontSmem<M>& sm, const uint32_t (&w)[Fr
     front_child<M>(sm, w, j, c);
     front_store<M>(dst, c);
     dst += FrontGeom<M>::VPN;
+  }
+}
+
+// Position of the k-th (0-based) set bit of x, k < popcount(x): a 5-step binary
+// search on popcounts of the low halves (no loop over the bits).
+__device__ inline int kth_bit(uint32_t x, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 16; w; w >>= 1) {
+    const uint32_t lo = x & ((1u << w) - 1u);
+    const int c = __popc(lo);
+    const bool up = k >= c;
+    k = up ? k - c : k;
+    x = up ? (x >> w) : lo;
+    pos += up ? w : 0;
+  }
+  return pos;
+}
+
+// Child-parallel expansion of n nodes staged in LDS (src[i], one per node): ONE
+// THREAD PER CHILD instead of one per parent. In a narrow window a thread-per-parent
+// expansion runs its parent's ~20 children one after the other (two dependent passes
+// of LDS row reads and max-plus chains per child: ~2.7 us per tree level on
+// MI355X) while most lanes idle; here child c finds its parent (binary search on the
+// child offsets), its job (k-th unscheduled bit) and the parent's remain (the
+// parent's unscheduled rows summed as packed u16 pairs: every row read is
+// independent, all of them issued together), then bounds itself. Leaves lower the
+// incumbent and are counted in nleaf; survivors are compacted (block scan) and
+// handed to store(index, child words). Returns the survivor count. Every thread
+// calls it (block-wide scans).
+template <int M, class Store>
+__device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const uint4 (*src)[FrontGeom<M>::VPN],
+                                      int n, int best, int& nleaf, Store store) {
+  using G = FrontGeom<M>;
+  constexpr int HW = (M + 1) / 2;  // packed u16 pairs of one p row / remain
+  const int tid = threadIdx.x;
+  int T = 0;
+  const int off = block_exclusive_scan(tid < n ? __popc(src[tid][0].y) : 0, sm.scan, &T);
+  if (tid < n) sm.coff[tid] = off;
+  __syncthreads();
+  int nout = 0;
+  for (int cb = 0; cb < T; cb += kBlock) {
+    const int c = cb + tid;
+    bool surv = false;
+    int j = 0;
+    uint32_t w[G::NW];
+#pragma unroll
+    for (int i = 0; i < G::NW; ++i) w[i] = 0;
+    if (c < T) {
+      int lo = 0, hi = n - 1;  // last node whose children start at or before c
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sm.coff[mid] <= c)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+#pragma unroll
+      for (int q = 0; q < G::VPN; ++q) {
+        const uint4 x = src[lo][q];
+        w[4 * q] = x.x;
+        w[4 * q + 1] = x.y;
+        w[4 * q + 2] = x.z;
+        w[4 * q + 3] = x.w;
+      }
+      const uint32_t rest = w[1];
+      j = kth_bit(rest, c - sm.coff[lo]);
+      // remain of the parent: rows of its unscheduled jobs (rows past a.jobs are 0)
+      uint32_t r2[HW];
+#pragma unroll
+      for (int h = 0; h < HW; ++h) r2[h] = 0;
+#pragma unroll
+      for (int jj = 0; jj < G::NJ; ++jj) {
+        const uint4* r4 = reinterpret_cast<const uint4*>(sm.ptab[jj]);
+        const uint32_t sel = ((rest >> jj) & 1u) ? 0xffffffffu : 0u;
+#pragma unroll
+        for (int q = 0; q < G::RV; ++q) {
+          const uint4 x = r4[q];
+          const uint32_t xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (4 * q + e < HW) r2[4 * q + e] += xv[e] & sel;  // sums < 65536: no carry (pfsp_front_ok)
+        }
+      }
+      int pr[M];
+      front_row<M>(sm.ptab[j], pr);
+      auto rem = [&](int m) { return static_cast<int>((r2[m >> 1] >> ((m & 1) * 16)) & 0xffffu) + a.min_tails[m]; };
+      const int f0 = front_of<M>(w, 0);
+      int lb = f0 + rem(0);
+      int tt = f0 + pr[0];
+#pragma unroll
+      for (int m = 1; m < M; ++m) {
+        const int sv = max(tt, front_of<M>(w, m));
+        lb = max(lb, sv + rem(m));
+        tt = sv + pr[m];
+      }
+      if (static_cast<int>(w[0] & 0xffu) + 1 == a.jobs) {
+        ++nleaf;
+        if (lb < best) atomicMin(&a.pool.ctl->best.v, lb);
+      } else {
+        surv = lb < best;
+      }
+    }
+    int tot = 0;
+    const int idx = nout + block_exclusive_scan(surv ? 1 : 0, sm.scan, &tot);
+    if (surv) {
+      uint32_t cw[G::NW];
+      front_child<M>(sm, w, j, cw);
+      store(idx, cw);
+    }
+    nout += tot;
+  }
+  return nout;
+}
+
+// Two-level chunk, child-parallel (default): the chunk's BPF parents go to LDS, their
+// children (<= BPF x 19 <= kBlock survivors) are expanded one per thread into sm.mid,
+// then the survivors' children one per thread into the chunk's slot region. Same
+// counts as front_two_level: level-1 survivors are pushed-and-expanded tree nodes
+// (high half of the leaf word), level-2 survivors the chunk's output.
+template <int M>
+__device__ inline void front_two_level_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t,
+                                          int best) {
+  using G = FrontGeom<M>;
+  using Node = PfspFrontNode<M>;
+  static_assert(G::BPF * (G::NJ - 1) <= kBlock, "level-1 survivors must fit sm.mid");
+  const int tid = threadIdx.x;
+  const auto& pa = a.pool;
+  Node* const bout = pa.buf[(t & 1) ^ 1];
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+    const u64 g0 = static_cast<u64>(ch) * G::BPF;
+    const int n0 = static_cast<int>(min(static_cast<u64>(G::BPF), v.B - g0));
+    if (tid < n0 * G::VPN) {
+      const int i = tid / G::VPN, q = tid - (tid / G::VPN) * G::VPN;
+      sm.par[i][q] = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + i, sm.pool))[q];
+    }
+    __syncthreads();
+    int nleaf = 0;
+    const int n1 = front_expand_cp<M>(a, sm, sm.par, n0, best, nleaf,
+                                      [&](int i, const uint32_t (&c)[G::NW]) { front_store<M>(&sm.mid[i][0], c); });
+    __syncthreads();  // level-1 survivors visible
+    uint4* const out = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
+    const int n2 = front_expand_cp<M>(a, sm, sm.mid, n1, best, nleaf,
+                                      [&](int i, const uint32_t (&c)[G::NW]) { front_store<M>(out + i * G::VPN, c); });
+    int leaves = 0;
+    (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
+    if (tid == 0) {
+      cnt_out[ch] = n2;
+      lcnt_out[ch] = leaves | (n1 << 16);
+    }
+    __syncthreads();  // sm.par / sm.mid / sm.coff are rewritten by the next chunk
   }
 }
 
@@ -335,10 +493,11 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, G::BPF, G::LT);
   if (v.B == 0 || v.overflow) return;
   {
+    // rows past a.jobs are zero (the child-parallel remain reads every row)
     uint16_t* pt = &sm.ptab[0][0];
 #pragma unroll
     for (int i = 0; i < PTN; ++i)
-      if (tid + i * kBlock < a.jobs * G::MS) pt[tid + i * kBlock] = ptv[i];
+      if (tid + i * kBlock < G::NJ * G::MS) pt[tid + i * kBlock] = ptv[i];
   }
   const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   Node* const bout = pa.buf[(t & 1) ^ 1];
@@ -351,7 +510,10 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     return;
   }
   if (v.fused) {
-    front_two_level<M>(a, sm, v, t, best);
+    if (a.fused_cp)
+      front_two_level_cp<M>(a, sm, v, t, best);
+    else
+      front_two_level<M>(a, sm, v, t, best);
     return;
   }
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {

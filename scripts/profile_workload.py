@@ -84,6 +84,43 @@ elif which.startswith("spillbig"):  # spillbig[:seconds]: ta021 LB1_d begun from
     print(which, f"{len(nodes)} begin nodes, capacity {st['capacity']} nodes: {st['tree'] / dt / 1e9:.3f} G nodes/s "
           f"over {dt:.2f} s, spilled {st['spilled']} refilled {st['refilled']} pinned MB {st['pinned_bytes'] >> 20} "
           f"pool device {st['device_nodes']} host {st['host_nodes']}")
+    del eng
+    raise SystemExit(0)
+elif which.startswith("spill014"):  # spill014[:ring_MB]: ta014 LB1 solved to the end from a 400K-node host
+    # frontier on a 1024-parent window: with the smallest ring (1 MB -> its floor) most of the frontier
+    # waits in pinned host blocks and comes back through refills while replays run; golden tree checked
+    import time
+    parts = which.split(":")
+    ring = int(parts[1]) << 20 if len(parts) > 1 else 1 << 20
+    m = PfspModel(14, 1)
+    nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 400_000)
+    eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=ring))
+    ts = []
+    for rep in range(4):
+        eng.set_trace(rep == 3)  # the last solve records the replay / copy timeline
+        t0 = time.perf_counter()
+        eng.begin(nodes, int(best))
+        eng.run()
+        eng.synchronize()
+        ts.append(time.perf_counter() - t0)
+        st = eng.stats()
+        assert (st["tree"] + tree1, st["sol"] + sol1) == (2573652, 2648), (st["tree"] + tree1, st["sol"] + sol1)
+    print(which, f"{len(nodes)} begin nodes, capacity {st['capacity']} nodes: {min(ts[:3]) * 1e3:.2f} ms per solve "
+          f"(best of 3 untraced), spilled {st['spilled']} refilled {st['refilled']} (last solve), "
+          f"pinned MB {st['pinned_bytes'] >> 20}")
+    tr = eng.trace()
+    import numpy as np
+    g = tr[tr[:, 0] == 0][:, 1:]
+    for kind, name in ((1, "spill D2H"), (2, "refill H2D")):
+        c = tr[tr[:, 0] == kind][:, 1:]
+        tot = float((c[:, 1] - c[:, 0]).sum()) if len(c) else 0.0
+        ov = 0.0
+        for a, b in c:  # overlap with the union of replay intervals (replays are serial on one stream)
+            ov += float(np.clip(np.minimum(g[:, 1], b) - np.maximum(g[:, 0], a), 0, None).sum())
+        print(f"  {name}: {len(c)} copies (enqueue-to-complete spans), {tot:.3f} ms, {ov:.3f} ms "
+              f"({100 * ov / tot if tot else 0:.0f} %) while a graph replay ran")
+    print(f"  replays: {len(g)}, {float((g[:, 1] - g[:, 0]).sum()):.3f} ms; traced solve {ts[3] * 1e3:.2f} ms")
+    del eng
     raise SystemExit(0)
 elif which == "queens":
     m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=32 << 30))
