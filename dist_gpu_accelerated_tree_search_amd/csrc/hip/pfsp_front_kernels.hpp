@@ -40,8 +40,11 @@ struct FrontGeom {
   static constexpr int LT = 8;                          // local DFS steps per chunk at most
   static constexpr int SLOT = 2 * MAXCH;                // chunk slot region = its private stack
   static constexpr int MAXCHUNKS = 2048;
-  // two-level chunks: level-1 children one per thread, grandchildren within MAXCH
-  static constexpr int BPF = (kBlock / NJ) < (MAXCH / (NJ * (NJ - 1))) ? (kBlock / NJ) : (MAXCH / (NJ * (NJ - 1)));
+  // two-level chunks (front_two_level_cp): up to BPF_CP parents, spread over the grid
+  // (pool_begin); level-1 survivors past kBlock go out unexpanded, so the chunk's output
+  // stays within SLOT
+  static constexpr int BPF = 12;     // default cap: two-level windows up to 12 x 2048 parents
+  static constexpr int BPF_CP = 32;
   // u16 row stride of the LDS p table (as PfspConsts::MS): 16 B for M <= 8, else 48 B
   static constexpr int MS = M <= 8 ? 8 : 24;
   static constexpr int RV = (M + 7) / 8;                // 16-B vectors holding one row's M values
@@ -59,9 +62,7 @@ struct PfspFrontArgs {
   const int* offsets;
   int* bounds_out;
   int nparents;
-  // two-level iterations expand child-parallel (front_expand_cp, default) or one
-  // thread per parent (0, A/B runs: TTS_FUSED_CP=0)
-  int fused_cp;
+  int bpf;  // two-level chunks: at most this many parents (<= FrontGeom::BPF_CP)
 };
 
 template <int M>
@@ -70,7 +71,7 @@ struct FrontSmem {
   uint16_t ptab[G::NJ][G::MS];
   int scan[kBlock / kWave];
   uint4 mid[kBlock][G::VPN];  // level-1 survivors of a two-level chunk
-  uint4 par[G::BPF][G::VPN];  // a two-level chunk's parents (child-parallel expansion)
+  uint4 par[G::BPF_CP][G::VPN];  // a two-level chunk's parents (child-parallel expansion)
   int coff[kBlock];           // child offsets of the nodes being expanded (child-parallel)
   PoolSmem<G::MAXCHUNKS> pool;
 };
@@ -293,115 +294,51 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
   return nout;
 }
 
-// Two-level chunk, child-parallel (default): the chunk's BPF parents go to LDS, their
-// children (<= BPF x 19 <= kBlock survivors) are expanded one per thread into sm.mid,
-// then the survivors' children one per thread into the chunk's slot region. Same
-// counts as front_two_level: level-1 survivors are pushed-and-expanded tree nodes
-// (high half of the leaf word), level-2 survivors the chunk's output.
+// Two-level chunk, child-parallel (default): the chunk's v.bp parents go to LDS, their
+// children are expanded one per thread into sm.mid, then the survivors' children one
+// per thread into the chunk's slot region. Same counts as front_two_level: level-1
+// survivors expanded here are pushed-and-expanded tree nodes (high half of the leaf
+// word); level-1 survivors beyond sm.mid's kBlock nodes go out unexpanded (first in the
+// slot region) with the level-2 survivors as the chunk's output.
 template <int M>
 __device__ inline void front_two_level_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t,
                                           int best) {
   using G = FrontGeom<M>;
   using Node = PfspFrontNode<M>;
-  static_assert(G::BPF * (G::NJ - 1) <= kBlock, "level-1 survivors must fit sm.mid");
+  static_assert(G::BPF_CP * (G::NJ - 1) + kBlock * (G::NJ - 1) <= G::SLOT, "chunk output must fit its slot region");
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
-    const u64 g0 = static_cast<u64>(ch) * G::BPF;
-    const int n0 = static_cast<int>(min(static_cast<u64>(G::BPF), v.B - g0));
+    const u64 g0 = static_cast<u64>(ch) * v.bp;
+    const int n0 = static_cast<int>(min(static_cast<u64>(v.bp), v.B - g0));
     if (tid < n0 * G::VPN) {
       const int i = tid / G::VPN, q = tid - (tid / G::VPN) * G::VPN;
       sm.par[i][q] = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + i, sm.pool))[q];
     }
     __syncthreads();
     int nleaf = 0;
-    const int n1 = front_expand_cp<M>(a, sm, sm.par, n0, best, nleaf,
-                                      [&](int i, const uint32_t (&c)[G::NW]) { front_store<M>(&sm.mid[i][0], c); });
-    __syncthreads();  // level-1 survivors visible
     uint4* const out = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
-    const int n2 = front_expand_cp<M>(a, sm, sm.mid, n1, best, nleaf,
-                                      [&](int i, const uint32_t (&c)[G::NW]) { front_store<M>(out + i * G::VPN, c); });
+    const int n1 = front_expand_cp<M>(a, sm, sm.par, n0, best, nleaf, [&](int i, const uint32_t (&c)[G::NW]) {
+      if (i < kBlock)
+        front_store<M>(&sm.mid[i][0], c);
+      else
+        front_store<M>(out + (i - kBlock) * G::VPN, c);  // overflow: out unexpanded
+    });
+    __syncthreads();  // level-1 survivors visible
+    const int n1e = min(n1, kBlock), ovf = n1 - n1e;
+    const int n2 = front_expand_cp<M>(a, sm, sm.mid, n1e, best, nleaf, [&](int i, const uint32_t (&c)[G::NW]) {
+      front_store<M>(out + (ovf + i) * G::VPN, c);
+    });
     int leaves = 0;
     (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
     if (tid == 0) {
-      cnt_out[ch] = n2;
-      lcnt_out[ch] = leaves | (n1 << 16);
+      cnt_out[ch] = ovf + n2;
+      lcnt_out[ch] = leaves | (n1e << 16);
     }
     __syncthreads();  // sm.par / sm.mid / sm.coff are rewritten by the next chunk
-  }
-}
-
-// Two-level chunk loop (v.fused): BPF parents per chunk, one per thread of the first
-// wave, expanded into LDS (level 1: those survivors are pushed-and-popped tree nodes,
-// counted in the high half of the chunk's leaf word), then every level-1 survivor —
-// one per thread — is expanded and its survivors go to the chunk's slot region.
-template <int M>
-__device__ inline void front_two_level(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t,
-                                       int best) {
-  using G = FrontGeom<M>;
-  using Node = PfspFrontNode<M>;
-  const int tid = threadIdx.x;
-  const auto& pa = a.pool;
-  Node* const bout = pa.buf[(t & 1) ^ 1];
-  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
-  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
-    uint32_t w[G::NW];
-#pragma unroll
-    for (int i = 0; i < G::NW; ++i) w[i] = 0;
-    const u64 gi = static_cast<u64>(ch) * G::BPF + tid;
-    if (tid < G::BPF && gi < v.B) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
-    uint32_t surv = 0;
-    int nsurv = 0, nleaf = 0;
-    const bool leaf1 = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-    front_parent<M>(a, sm, w, [&](int j, int lb) {
-      if (leaf1) {
-        ++nleaf;
-        if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-      } else if (lb < best) {
-        ++nsurv;
-        surv |= 1u << j;
-      }
-    });
-    int tot1 = 0;
-    const int off1 = block_exclusive_scan(nsurv, sm.scan, &tot1);
-    front_emit<M>(sm, w, surv, &sm.mid[off1][0]);
-    __syncthreads();
-    surv = 0;
-    nsurv = 0;
-#pragma unroll
-    for (int i = 0; i < G::NW; ++i) w[i] = 0;
-    if (tid < tot1) {
-#pragma unroll
-      for (int q = 0; q < G::VPN; ++q) {
-        const uint4 x = sm.mid[tid][q];
-        w[4 * q] = x.x;
-        w[4 * q + 1] = x.y;
-        w[4 * q + 2] = x.z;
-        w[4 * q + 3] = x.w;
-      }
-    }
-    const bool leaf2 = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-    front_parent<M>(a, sm, w, [&](int j, int lb) {
-      if (leaf2) {
-        ++nleaf;
-        if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-      } else if (lb < best) {
-        ++nsurv;
-        surv |= 1u << j;
-      }
-    });
-    int tot = 0;
-    const int off = block_exclusive_scan(nsurv | (nleaf << 16), sm.scan, &tot) & 0xffff;
-    if (tid == 0) {
-      cnt_out[ch] = tot & 0xffff;
-      lcnt_out[ch] = (tot >> 16) | (tot1 << 16);
-    }
-    front_emit<M>(sm, w, surv, reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off));
-    __syncthreads();  // sm.mid is rewritten by the next chunk
   }
 }
 
@@ -474,6 +411,8 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
 // Occupancy: the iterations are latency-bound (the per-child chain, LDS row reads), so
 // the register budget is capped for more resident waves: 6 per SIMD up to 10 machines,
 // 4 for 20 (f, remain and a p row stay in registers without scratch).
+// (8 waves per SIMD for M <= 10, SGPRs spilled to VGPR lanes, measured: ta014 +2 %,
+// ta008 -4 %; not kept, profiles/r3/probes/front_w8_ab.txt)
 template <int M>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 10 ? 6 : 4)))
 void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
@@ -490,7 +429,7 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     const int x = tid + i * kBlock;
     ptv[i] = x < a.jobs * G::MS ? a.ptab[x] : 0;
   }
-  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, G::BPF, G::LT);
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, a.bpf, G::LT);
   if (v.B == 0 || v.overflow) return;
   {
     // rows past a.jobs are zero (the child-parallel remain reads every row)
@@ -510,10 +449,7 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     return;
   }
   if (v.fused) {
-    if (a.fused_cp)
-      front_two_level_cp<M>(a, sm, v, t, best);
-    else
-      front_two_level<M>(a, sm, v, t, best);
+    front_two_level_cp<M>(a, sm, v, t, best);
     return;
   }
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {

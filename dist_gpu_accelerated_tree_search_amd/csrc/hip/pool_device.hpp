@@ -229,7 +229,13 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   const bool bad_split = armed && v.B < v.S + v.C;
   v.split = armed && !bad_split && v.B >= split_min;
   v.fused = !v.local && BPF > 0 && !armed && v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
-  int bp = v.fused ? BPF : BP;
+  int bp = BP;
+  if (v.fused) {
+    // up to BPF parents per two-level chunk, fewer when the window is narrower than the
+    // grid: more workgroups share a narrow window (each with fewer serial passes)
+    const u64 per = (v.B + gridDim.x - 1) / gridDim.x;
+    bp = static_cast<int>(min(static_cast<u64>(BPF), max(per, 1ull)));
+  }
   if (v.local) {
     // spread a window smaller than the grid over every workgroup
     const u64 per = (v.B + gridDim.x - 1) / gridDim.x;

@@ -30,6 +30,26 @@ def test_pinned_spill_and_refill_keep_the_tree(ub, frontier, window):
     assert st["host_nodes"] == 0 and st["device_nodes"] == 0
 
 
+def test_trace_records_replays_and_pool_copies():
+    # engine.set_trace / engine.trace (csrc/hip/engine.hpp): timing events around every
+    # graph replay (kind 0), spill D2H (1) and refill H2D (2); the forced-spill solve
+    # keeps the golden tree, and every interval is well-formed
+    model = PfspModel(14, 1)
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1024, ring_bytes=1 << 20))
+    eng.set_trace(True)
+    r = solve_engine(model, eng, ub=1, m=300_000)
+    assert (r.tree, r.sol, r.best) == GOLD14
+    tr = eng.trace()
+    assert tr.ndim == 2 and tr.shape[1] == 3 and len(tr) > 0
+    kinds = set(tr[:, 0].astype(int).tolist())
+    assert {0, 2} <= kinds, kinds  # replays and refills (the frontier starts in pinned blocks)
+    assert (tr[:, 2] >= tr[:, 1]).all() and (tr[:, 1] >= 0).all()
+    eng.set_trace(False)
+    r = solve_engine(model, eng, ub=1, m=25)
+    assert (r.tree, r.sol, r.best) == GOLD14
+    assert len(eng.trace()) == 0
+
+
 def test_export_import_between_engines_keeps_the_tree():
     import torch
 
