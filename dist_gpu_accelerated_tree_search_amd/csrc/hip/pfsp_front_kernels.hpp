@@ -45,6 +45,8 @@ struct FrontGeom {
   // stays within SLOT
   static constexpr int BPF = 12;     // default cap: two-level windows up to 12 x 2048 parents
   static constexpr int BPF_CP = 32;
+  static constexpr int MID = M > 10 ? 96 : 128;  // level-1 survivors expanded in place (the rest go out)
+  static constexpr int HW = (M + 1) / 2;  // packed u16 pairs of a p row / a remain
   // u16 row stride of the LDS p table (as PfspConsts::MS): 16 B for M <= 8, else 48 B
   static constexpr int MS = M <= 8 ? 8 : 24;
   static constexpr int RV = (M + 7) / 8;                // 16-B vectors holding one row's M values
@@ -70,9 +72,14 @@ struct FrontSmem {
   using G = FrontGeom<M>;
   uint16_t ptab[G::NJ][G::MS];
   int scan[kBlock / kWave];
-  uint4 mid[kBlock][G::VPN];  // level-1 survivors of a two-level chunk
-  uint4 par[G::BPF_CP][G::VPN];  // a two-level chunk's parents (child-parallel expansion)
-  int coff[kBlock];           // child offsets of the nodes being expanded (child-parallel)
+  // two-level chunks (child-parallel expansion): the chunk's parents and the level-1
+  // survivors expanded in place, each with its remain (unscheduled work per machine,
+  // packed u16 pairs), and the child offsets of the nodes being expanded
+  uint4 par[G::BPF_CP][G::VPN];
+  uint32_t rpar[G::BPF_CP][G::HW];
+  uint4 mid[G::MID][G::VPN];
+  uint32_t rmid[G::MID][G::HW];
+  int coff[G::MID];
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -198,22 +205,20 @@ __device__ inline int kth_bit(uint32_t x, int k) {
   return pos;
 }
 
-// Child-parallel expansion of n nodes staged in LDS (src[i], one per node): ONE
-// THREAD PER CHILD instead of one per parent. In a narrow window a thread-per-parent
-// expansion runs its parent's ~20 children one after the other (two dependent passes
-// of LDS row reads and max-plus chains per child: ~2.7 us per tree level on
-// MI355X) while most lanes idle; here child c finds its parent (binary search on the
-// child offsets), its job (k-th unscheduled bit) and the parent's remain (the
-// parent's unscheduled rows summed as packed u16 pairs: every row read is
-// independent, all of them issued together), then bounds itself. Leaves lower the
-// incumbent and are counted in nleaf; survivors are compacted (block scan) and
-// handed to store(index, child words). Returns the survivor count. Every thread
-// calls it (block-wide scans).
+// Child-parallel expansion of n nodes staged in LDS (src[i], with their remain
+// rem[i]): ONE THREAD PER CHILD instead of one per parent. In a narrow window a
+// thread-per-parent expansion runs its parent's ~20 children one after the other while
+// most lanes idle; here child c finds its parent (binary search on the child offsets)
+// and its job (k-th unscheduled bit), then bounds itself from the parent's front and
+// remain (no pass over the parent's rows: remains are carried, a child's is its
+// parent's minus its own row). Leaves lower the incumbent and are counted in nleaf;
+// survivors are compacted (block scan) and handed to store(index, child words, child
+// remain). Returns the survivor count. Every thread calls it (block-wide scans).
 template <int M, class Store>
 __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const uint4 (*src)[FrontGeom<M>::VPN],
-                                      int n, int best, int& nleaf, Store store) {
+                                      const uint32_t (*rem)[FrontGeom<M>::HW], int n, int best, int& nleaf, Store store) {
   using G = FrontGeom<M>;
-  constexpr int HW = (M + 1) / 2;  // packed u16 pairs of one p row / remain
+  constexpr int HW = G::HW;
   const int tid = threadIdx.x;
   int T = 0;
   const int off = block_exclusive_scan(tid < n ? __popc(src[tid][0].y) : 0, sm.scan, &T);
@@ -224,9 +229,11 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
     const int c = cb + tid;
     bool surv = false;
     int j = 0;
-    uint32_t w[G::NW];
+    uint32_t w[G::NW], cr[HW];
 #pragma unroll
     for (int i = 0; i < G::NW; ++i) w[i] = 0;
+#pragma unroll
+    for (int h = 0; h < HW; ++h) cr[h] = 0;
     if (c < T) {
       int lo = 0, hi = n - 1;  // last node whose children start at or before c
       while (lo < hi) {
@@ -244,36 +251,24 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
         w[4 * q + 2] = x.z;
         w[4 * q + 3] = x.w;
       }
-      const uint32_t rest = w[1];
-      j = kth_bit(rest, c - sm.coff[lo]);
-      // remain of the parent: rows of its unscheduled jobs (rows past a.jobs are 0)
-      uint32_t r2[HW];
+      j = kth_bit(w[1], c - sm.coff[lo]);
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
+      uint32_t pw[HW];
 #pragma unroll
-      for (int h = 0; h < HW; ++h) r2[h] = 0;
-#pragma unroll
-      for (int jj = 0; jj < G::NJ; ++jj) {
-        const uint4* r4 = reinterpret_cast<const uint4*>(sm.ptab[jj]);
-        const uint32_t sel = ((rest >> jj) & 1u) ? 0xffffffffu : 0u;
-#pragma unroll
-        for (int q = 0; q < G::RV; ++q) {
-          const uint4 x = r4[q];
-          const uint32_t xv[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (4 * q + e < HW) r2[4 * q + e] += xv[e] & sel;  // sums < 65536: no carry (pfsp_front_ok)
-        }
+      for (int h = 0; h < HW; ++h) {
+        pw[h] = row[h];
+        cr[h] = rem[lo][h] - pw[h];  // the child's remain (packed halves never borrow: row <= remain)
       }
-      int pr[M];
-      front_row<M>(sm.ptab[j], pr);
-      auto rem = [&](int m) { return static_cast<int>((r2[m >> 1] >> ((m & 1) * 16)) & 0xffffu) + a.min_tails[m]; };
+      auto pm = [&](int m) { return static_cast<int>((pw[m >> 1] >> ((m & 1) * 16)) & 0xffffu); };
+      auto rm = [&](int m) { return static_cast<int>((rem[lo][m >> 1] >> ((m & 1) * 16)) & 0xffffu) + a.min_tails[m]; };
       const int f0 = front_of<M>(w, 0);
-      int lb = f0 + rem(0);
-      int tt = f0 + pr[0];
+      int lb = f0 + rm(0);
+      int tt = f0 + pm(0);
 #pragma unroll
       for (int m = 1; m < M; ++m) {
         const int sv = max(tt, front_of<M>(w, m));
-        lb = max(lb, sv + rem(m));
-        tt = sv + pr[m];
+        lb = max(lb, sv + rm(m));
+        tt = sv + pm(m);
       }
       if (static_cast<int>(w[0] & 0xffu) + 1 == a.jobs) {
         ++nleaf;
@@ -287,7 +282,7 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
     if (surv) {
       uint32_t cw[G::NW];
       front_child<M>(sm, w, j, cw);
-      store(idx, cw);
+      store(idx, cw, cr);
     }
     nout += tot;
   }
@@ -305,7 +300,8 @@ __device__ inline void front_two_level_cp(const PfspFrontArgs<M>& a, FrontSmem<M
                                           int best) {
   using G = FrontGeom<M>;
   using Node = PfspFrontNode<M>;
-  static_assert(G::BPF_CP * (G::NJ - 1) + kBlock * (G::NJ - 1) <= G::SLOT, "chunk output must fit its slot region");
+  static_assert(G::BPF_CP * (G::NJ - 1) + G::MID * (G::NJ - 1) <= G::SLOT, "chunk output must fit its slot region");
+  static_assert(G::MID <= kBlock && G::BPF_CP <= kBlock, "one thread per staged node");
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   Node* const bout = pa.buf[(t & 1) ^ 1];
@@ -314,24 +310,42 @@ __device__ inline void front_two_level_cp(const PfspFrontArgs<M>& a, FrontSmem<M
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 g0 = static_cast<u64>(ch) * v.bp;
     const int n0 = static_cast<int>(min(static_cast<u64>(v.bp), v.B - g0));
-    if (tid < n0 * G::VPN) {
-      const int i = tid / G::VPN, q = tid - (tid / G::VPN) * G::VPN;
-      sm.par[i][q] = reinterpret_cast<const uint4*>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + i, sm.pool))[q];
+    if (tid < n0) {
+      // the parent's remain: one pass over its unscheduled rows (packed u16 pairs; sums
+      // < 65536, pfsp_front_ok), by the thread that stages it
+      uint32_t w[G::NW];
+      front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
+      front_store<M>(&sm.par[tid][0], w);
+      uint32_t r2[G::HW];
+#pragma unroll
+      for (int h = 0; h < G::HW; ++h) r2[h] = 0;
+      for (uint32_t x = w[1]; x; x &= x - 1) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[__builtin_ctz(x)]);
+#pragma unroll
+        for (int h = 0; h < G::HW; ++h) r2[h] += row[h];
+      }
+#pragma unroll
+      for (int h = 0; h < G::HW; ++h) sm.rpar[tid][h] = r2[h];
     }
     __syncthreads();
     int nleaf = 0;
     uint4* const out = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
-    const int n1 = front_expand_cp<M>(a, sm, sm.par, n0, best, nleaf, [&](int i, const uint32_t (&c)[G::NW]) {
-      if (i < kBlock)
-        front_store<M>(&sm.mid[i][0], c);
-      else
-        front_store<M>(out + (i - kBlock) * G::VPN, c);  // overflow: out unexpanded
-    });
+    const int n1 = front_expand_cp<M>(a, sm, sm.par, sm.rpar, n0, best, nleaf,
+                                      [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {
+                                        if (i < G::MID) {
+                                          front_store<M>(&sm.mid[i][0], c);
+#pragma unroll
+                                          for (int h = 0; h < G::HW; ++h) sm.rmid[i][h] = r[h];
+                                        } else {
+                                          front_store<M>(out + (i - G::MID) * G::VPN, c);  // out unexpanded
+                                        }
+                                      });
     __syncthreads();  // level-1 survivors visible
-    const int n1e = min(n1, kBlock), ovf = n1 - n1e;
-    const int n2 = front_expand_cp<M>(a, sm, sm.mid, n1e, best, nleaf, [&](int i, const uint32_t (&c)[G::NW]) {
-      front_store<M>(out + (ovf + i) * G::VPN, c);
-    });
+    const int n1e = min(n1, G::MID), ovf = n1 - n1e;
+    const int n2 = front_expand_cp<M>(a, sm, sm.mid, sm.rmid, n1e, best, nleaf,
+                                      [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&)[G::HW]) {
+                                        front_store<M>(out + (ovf + i) * G::VPN, c);
+                                      });
     int leaves = 0;
     (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
     if (tid == 0) {
@@ -432,7 +446,6 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, a.bpf, G::LT);
   if (v.B == 0 || v.overflow) return;
   {
-    // rows past a.jobs are zero (the child-parallel remain reads every row)
     uint16_t* pt = &sm.ptab[0][0];
 #pragma unroll
     for (int i = 0; i < PTN; ++i)
