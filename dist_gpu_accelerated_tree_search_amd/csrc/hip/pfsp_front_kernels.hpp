@@ -443,7 +443,7 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     const int x = tid + i * kBlock;
     ptv[i] = x < a.jobs * G::MS ? a.ptab[x] : 0;
   }
-  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, a.bpf, G::LT);
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, a.bpf, G::LT, G::NJ * (G::NJ - 1));
   if (v.B == 0 || v.overflow) return;
   {
     uint16_t* pt = &sm.ptab[0][0];

@@ -170,7 +170,7 @@ template <class Node, int MAXCHUNKS>
 // levels; what is left on the stack is the chunk's output. Several tree levels per
 // dependent kernel, and the next iteration re-deals the stacks over the grid.
 __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, PoolSmem<MAXCHUNKS>& ps,
-                                      int BPF = 0, int LT = 1) {
+                                      int BPF = 0, int LT = 1, int GROW2 = 0) {
   const int s_in = t % 3, s_out = (t + 1) % 3;
   const int b_in = t & 1;
   PoolCtl* ctl = pa.ctl;
@@ -228,13 +228,22 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // a pending split needs the whole (replicated) pool inside the window
   const bool bad_split = armed && v.B < v.S + v.C;
   v.split = armed && !bad_split && v.B >= split_min;
-  v.fused = !v.local && BPF > 0 && !armed && v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
+  // Two-level iterations also run while a rank split is armed (the replicated prefix
+  // of a multi-rank solve), but never as the split iteration itself, and only while
+  // two levels of growth (at most GROW2 grandchildren per parent) cannot carry the
+  // pool past the parent window before the split.
+  const bool fuse_armed = armed && !(v.B >= split_min) &&
+                          v.B * static_cast<u64>(max(GROW2, 1)) <= static_cast<u64>(pa.max_parents) && GROW2 > 0;
+  v.fused = !v.local && BPF > 0 && (!armed || fuse_armed) &&
+            v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
   int bp = BP;
   if (v.fused) {
     // up to BPF parents per two-level chunk, fewer when the window is narrower than the
-    // grid: more workgroups share a narrow window (each with fewer serial passes)
+    // grid: more workgroups share a narrow window (each with fewer serial passes). While
+    // a split is armed the pool order must not depend on the grid (every rank deals the
+    // same frontier by position), so those chunks keep BPF parents.
     const u64 per = (v.B + gridDim.x - 1) / gridDim.x;
-    bp = static_cast<int>(min(static_cast<u64>(BPF), max(per, 1ull)));
+    bp = armed ? BPF : static_cast<int>(min(static_cast<u64>(BPF), max(per, 1ull)));
   }
   if (v.local) {
     // spread a window smaller than the grid over every workgroup
