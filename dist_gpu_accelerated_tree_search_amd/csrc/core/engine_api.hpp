@@ -29,7 +29,6 @@ struct EngineConfig {
   int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
   int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
   bool use_graphs = true;
-  bool window_grid = false;              // cap the window at one chunk per resident workgroup
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };
 

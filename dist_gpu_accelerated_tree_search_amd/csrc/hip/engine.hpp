@@ -60,14 +60,10 @@ class DeviceEngine final : public IEngine {
     int per_cu = std::max(1, Traits::blocks_per_cu());
     if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(g));  // tuning
     const size_t resident = static_cast<size_t>(cus) * per_cu;
-    // the parent window is a whole number of chunks, at most kMaxChunks of them; with
-    // window_grid, no more chunks than resident workgroups (a window of 2048 chunks on
-    // 1792 resident workgroups runs its last 256 chunks as a second pass)
+    // the parent window is a whole number of chunks, at most kMaxChunks of them (capping
+    // it at one chunk per resident workgroup measured no gain: profiles/r3/probes/window*)
     const size_t bp = Traits::kParentsPerChunk;
     max_chunks_ = std::min<size_t>((cfg_.max_parents + bp - 1) / bp, Traits::kMaxChunks);
-    bool window_grid = cfg_.window_grid;
-    if (const char* f = std::getenv("TTS_WINDOW_GRID")) window_grid = std::atoi(f) != 0;  // A/B runs
-    if (window_grid) max_chunks_ = std::max<size_t>(1, std::min(max_chunks_, resident));
     cfg_.max_parents = max_chunks_ * bp;
     buf_nodes_ = max_chunks_ * static_cast<size_t>(Traits::kChildrenPerChunk);
     size_t cap = 1;
