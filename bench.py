@@ -112,9 +112,16 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    comm = Comm(use_gpu=(a.backend == "gpu" and a.comm == "nccl"), device=a.device)
+    # a failed RCCL point-to-point preflight is reported (stderr and the JSON line) and the
+    # run continues WITHOUT node transfers (static in-search split, ref -w 0 -L 0), so the
+    # numbers that need no transfer are still measured
+    comm = Comm(use_gpu=(a.backend == "gpu" and a.comm == "nccl"), device=a.device, preflight_raise=False)
     if comm.preflight is not None:
-        log(f"rank {comm.rank}: RCCL point-to-point preflight ok: {comm.preflight}")
+        log(f"rank {comm.rank}: RCCL point-to-point preflight: {comm.preflight}")
+    if not comm.p2p_ok:
+        log(f"rank {comm.rank}: point-to-point transfers FAILED the preflight on some rank: "
+            "running without work sharing (static partition)")
+        a.no_ws = True
     model = PfspModel(a.inst, a.lb)
     opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * (1 << 30)))
     device = (comm.topo.local_rank if a.device is None else a.device) if a.backend == "gpu" else 0
@@ -176,6 +183,7 @@ def main() -> int:
             "rounds_last_step": last.extra.get("rounds"),
             "baseline": "reference pfsp_omp_c.out -C 8 -l 0, 23 M nodes/s (BASELINE.md, same tree)",
             "p2p_preflight": comm.preflight,
+            "p2p_ok": comm.p2p_ok,
         },
     }
     del solver, engine

@@ -62,7 +62,7 @@ class Comm:
     """Process-group wrapper; world == 1 works without any process group."""
 
     def __init__(self, backend: str | None = None, use_gpu: bool = True, timeout_s: float = 1800.0,
-                 device: int | None = None):
+                 device: int | None = None, preflight_raise: bool = True):
         import torch
         import torch.distributed as dist
 
@@ -99,10 +99,38 @@ class Comm:
         if shm_control_wanted(self.topo):
             self.ctl = self._open_shm_control()
         self.preflight = None
-        if self.distributed and use_gpu and self.backend == "nccl":
-            self._connect_peers()
-            if os.environ.get("TTS_P2P_PREFLIGHT", "1") != "0":
-                self.preflight = self.preflight_p2p()
+        self.p2p_ok = True
+        # fault injection (like TTS_FAULT_*): the preflight runs on any backend and the
+        # data this rank receives is corrupted
+        fault = os.environ.get("TTS_FAULT_P2P_RANK")
+        if self.distributed and ((use_gpu and self.backend == "nccl") or fault not in (None, "")):
+            try:
+                if use_gpu and self.backend == "nccl":
+                    self._connect_peers()
+                if fault not in (None, "") and int(fault) == self.rank:
+                    real = self._p2p
+
+                    def corrupt(outgoing, incoming, src, dst, nb):
+                        real(outgoing, incoming, src, dst, nb)
+                        if dst is not None and dst.numel():
+                            dst[0] ^= 1
+
+                    self._p2p = corrupt
+                    try:
+                        self.preflight = self.preflight_p2p()
+                    finally:
+                        self._p2p = real
+                elif os.environ.get("TTS_P2P_PREFLIGHT", "1") != "0" or fault not in (None, ""):
+                    self.preflight = self.preflight_p2p()
+            except Exception as e:  # noqa: BLE001 - re-raised unless the caller takes it
+                if preflight_raise:
+                    raise
+                # every rank learns that some rank's point-to-point path failed; the caller
+                # runs without node transfers (static partition) and reports the failure
+                self.preflight = {"ok": False, "error": repr(e)[:300]}
+        if self.distributed and not preflight_raise:
+            mine = 1 if (self.preflight is None or self.preflight.get("ok")) else 0
+            self.p2p_ok = bool(self.allreduce_i64([mine], "min")[0])
 
     def preflight_p2p(self, nbytes: int = 4 << 20) -> dict:
         """Check the node-transfer path end to end before any solve relies on it.

@@ -110,6 +110,21 @@ def test_bench_extras_cpu_gloo():
     assert ex["ta056"]["time_box_s"] == 0.5
 
 
+def test_bench_runs_without_transfers_after_failed_preflight():
+    # a rank whose point-to-point check fails (fault injection): bench.py reports it in
+    # the JSON line and measures the headline without work sharing (static split), golden
+    env = dict(os.environ, TTS_FAULT_P2P_RANK="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--backend", "cpu", "--no-extras"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec["config"]["p2p_ok"] is False and rec["config"]["parallelism"] == "dp2"
+    assert (rec["config"]["tree"], rec["config"]["sol"], rec["config"]["makespan"]) == GOLD
+    assert "FAILED the preflight" in p.stderr
+
+
 def test_bench_extras_failure_still_prints_headline():
     # an extra that fails is reported in the line; the headline is printed regardless
     cmd = [sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--backend", "cpu", "--extras", "nosuch"]
