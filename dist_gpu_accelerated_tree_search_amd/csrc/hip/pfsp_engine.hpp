@@ -94,8 +94,6 @@ inline std::vector<uint16_t> pfsp_front_fill_args(const PfspInstance& in, dev::P
     for (int m = 0; m < in.machines; ++m) ptab[static_cast<size_t>(j) * MS + m] = static_cast<uint16_t>(in.pt(m, j));
   a.jobs = in.jobs;
   for (int m = 0; m < M; ++m) a.min_tails[m] = t.tails[m];
-  a.xcd = 1;
-  if (const char* f = std::getenv("TTS_XCD")) a.xcd = std::atoi(f) != 0;  // A/B runs
   a.bpf = dev::FrontGeom<M>::BPF;
   if (const char* f = std::getenv("TTS_FUSED_BPF"))  // A/B runs
     a.bpf = std::min(std::max(1, std::atoi(f)), dev::FrontGeom<M>::BPF_CP);

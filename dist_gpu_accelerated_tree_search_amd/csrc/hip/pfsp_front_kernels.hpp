@@ -65,7 +65,6 @@ struct PfspFrontArgs {
   int* bounds_out;
   int nparents;
   int bpf;  // two-level chunks: at most this many parents (<= FrontGeom::BPF_CP)
-  int xcd;  // XCD-aware chunk order (chunk_of_block)
 };
 
 template <int M>
@@ -308,10 +307,7 @@ __device__ inline void front_two_level_cp(const PfspFrontArgs<M>& a, FrontSmem<M
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  for (int base = 0; base < v.nchunks; base += gridDim.x) {
-    const int cb0 = chunk_of_block(blockIdx.x, gridDim.x, min(static_cast<int>(gridDim.x), v.nchunks - base), a.xcd);
-    if (cb0 < 0) continue;
-    const int ch = base + cb0;
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 g0 = static_cast<u64>(ch) * v.bp;
     const int n0 = static_cast<int>(min(static_cast<u64>(v.bp), v.B - g0));
     if (tid < n0) {
@@ -376,10 +372,7 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  for (int base = 0; base < v.nchunks; base += gridDim.x) {
-    const int cb0 = chunk_of_block(blockIdx.x, gridDim.x, min(static_cast<int>(gridDim.x), v.nchunks - base), a.xcd);
-    if (cb0 < 0) continue;
-    const int ch = base + cb0;
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     Node* const stk = bout + static_cast<size_t>(ch) * G::SLOT;
     int top = 0, pushed = 0, nleaf = 0;
     for (int s = 0; s < v.steps; ++s) {
@@ -472,10 +465,7 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     front_two_level_cp<M>(a, sm, v, t, best);
     return;
   }
-  for (int base = 0; base < v.nchunks; base += gridDim.x) {
-    const int cb0 = chunk_of_block(blockIdx.x, gridDim.x, min(static_cast<int>(gridDim.x), v.nchunks - base), a.xcd);
-    if (cb0 < 0) continue;
-    const int ch = base + cb0;
+  for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 gi = static_cast<u64>(ch) * G::BP + tid;
     uint32_t w[G::NW];
 #pragma unroll

@@ -288,19 +288,10 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   return v;
 }
 
-// XCD-aware chunk order. MI355X deals workgroup b to XCD b % 8, each XCD with its own
-// L2. In a pass over chunks [base, base + n), XCD x takes the contiguous range
-// [x*K, x*K + K), K = ceil(n / 8): consecutive chunks write neighbouring slices of the
-// next window, and the next iteration deals its window the same way, so a slice is
-// mostly re-read on the XCD whose L2 wrote it. Returns the chunk of block b in the pass
-// (or -1); identity when xcd is off or the grid is not a multiple of 8 (n <= g).
-__device__ inline int chunk_of_block(int b, int g, int n, bool xcd) {
-  if (!xcd || (g & 7)) return b < n ? b : -1;
-  const int K = (n + 7) >> 3;
-  const int i = b >> 3;
-  const int c = (b & 7) * K + i;
-  return (i < K && c < n) ? c : -1;
-}
+// (An XCD-aware chunk order — XCD x of the 8 taking a contiguous range of chunks, so a
+// slice of the pool is re-read through the L2 that wrote it — measured 1-5 % slower on
+// ta014 / ta008 / ta021: profiles/r3/probes/xcd_chunk_order_ab.txt. Chunk ch runs on
+// workgroup ch, dealt round-robin over the XCDs.)
 
 // Address of logical element i of the pool window read by this iteration:
 // buffer children first (top of the DFS stack), then the ring top.
