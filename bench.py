@@ -84,6 +84,10 @@ def main() -> int:
     ap.add_argument("--max-parents", type=int, default=1 << 19)
     ap.add_argument("--ring-gb", type=float, default=32.0)
     ap.add_argument("--init-per-rank", type=int, default=25)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="headline engines per GPU (csrc/core/multi_engine.hpp), the solve split between them")
+    ap.add_argument("--stream-split", type=int, default=512,
+                    help="with --streams > 1: parents per engine at the in-graph split")
     ap.add_argument("--no-ws", action="store_true", help="static partition (ref -w 0 / -L 0)")
     ap.add_argument("--backend", choices=["gpu", "cpu"], default="gpu")
     ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
@@ -123,7 +127,8 @@ def main() -> int:
             "running without work sharing (static partition)")
         a.no_ws = True
     model = PfspModel(a.inst, a.lb)
-    opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * (1 << 30)))
+    opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * (1 << 30)), streams=max(1, a.streams),
+                         stream_split=a.stream_split if a.streams > 1 else 0)
     device = (comm.topo.local_rank if a.device is None else a.device) if a.backend == "gpu" else 0
     engine = model.make_engine(a.backend, device, opts)
     cfg = DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws)

@@ -464,18 +464,20 @@ inline void bind_runner(py::module_& m, StagingFactory staging = {}, CpusOfDevic
       "Drive several engines (GPUs and/or CPU workers) from one process until all pools are empty.");
   m.def(
       "make_multi_engine",
-      [staging](py::list engines, size_t needy_below, size_t donor_min, size_t cap) -> std::unique_ptr<IEngine> {
+      [staging](py::list engines, size_t needy_below, size_t donor_min, size_t cap,
+                size_t split_min) -> std::unique_ptr<IEngine> {
         std::vector<IEngine*> es;
         for (auto e : engines) es.push_back(e.cast<IEngine*>());
         MultiConfig c;
         c.needy_below = std::max<size_t>(1, needy_below);
         c.donor_min = std::max<size_t>(2, donor_min);
         c.cap = std::max<size_t>(1, cap);
+        c.split_min = split_min;
         const bool dev = !es.empty() && es[0]->device() >= 0;
         return std::make_unique<MultiEngine>(std::move(es), dev && staging ? staging() : nullptr, c);
       },
       py::arg("engines"), py::arg("needy_below"), py::arg("donor_min"), py::arg("cap") = size_t(1) << 22,
-      py::keep_alive<0, 1>(),
+      py::arg("split_min") = size_t(0), py::keep_alive<0, 1>(),
       "Several engines on one device (one stream and one host thread each) as one engine: concurrent "
       "slices, same-device steal-half between slices (core/multi_engine.hpp).");
   m.def("parse_cpulist", &parse_cpulist);

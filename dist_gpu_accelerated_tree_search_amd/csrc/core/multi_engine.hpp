@@ -43,6 +43,11 @@ struct MultiConfig {
   size_t needy_below = 1;   // a sub-engine below this many nodes takes work between slices
   size_t donor_min = 2;     // a donor holds at least this many
   size_t cap = 1 << 22;     // at most this many nodes per hand-over
+  // > 0: every begin() splits the solve between the sub-engines in the graph (each
+  // begins from the same nodes; sub-engine k keeps share k of K once the replicated
+  // pool holds split_min * K parents, combined with a rank split as share rank * K + k
+  // of world * K), so K concurrent streams expand disjoint subtrees from the start
+  size_t split_min = 0;
 };
 
 class MultiEngine final : public IEngine {
@@ -139,6 +144,19 @@ class MultiEngine final : public IEngine {
   void import_device(const void* src, size_t n) override { e_[0]->import_device(src, n); }
 
   void begin(const void* nodes, size_t n, int best) override {
+    const int K = static_cast<int>(e_.size());
+    split_mode_ = cfg_.split_min > 0 && K > 1;
+    if (split_mode_) {
+      const int r = arm_ ? arank_ : 0, W = arm_ ? aworld_ : 1;
+      const size_t mp = std::max(arm_ ? amin_ / static_cast<size_t>(std::max(1, W)) : size_t(0), cfg_.split_min) *
+                        static_cast<size_t>(W * K);
+      for (int k = 0; k < K; ++k) {
+        e_[k]->set_split(r * K + k, W * K, mp);
+        e_[k]->begin(nodes, n, best);
+      }
+      arm_ = false;
+      return;
+    }
     e_[0]->begin(nodes, n, best);
     for (size_t i = 1; i < e_.size(); ++i) e_[i]->begin(nodes, 0, best);
   }
@@ -150,7 +168,16 @@ class MultiEngine final : public IEngine {
   size_t warm_split(int rank, int world, size_t window, int passes) override {
     return e_[0]->warm_split(rank, world, window, passes);
   }
-  void set_split(int rank, int world, size_t min_parents) override { e_[0]->set_split(rank, world, min_parents); }
+  void set_split(int rank, int world, size_t min_parents) override {
+    if (cfg_.split_min == 0 || e_.size() == 1) {
+      e_[0]->set_split(rank, world, min_parents);
+      return;
+    }
+    arm_ = true;  // applied by the next begin(), combined with the sub-engine split
+    arank_ = rank;
+    aworld_ = world;
+    amin_ = min_parents;
+  }
   bool split_pending() override { return e_[0]->split_pending(); }
 
   EngineStats stats() override {
@@ -183,7 +210,7 @@ class MultiEngine final : public IEngine {
     auto over = [&]() {
       return max_seconds > 0 && std::chrono::duration<double>(clock::now() - t0).count() >= max_seconds;
     };
-    if (e_.size() == 1 || e_[0]->split_pending()) {  // replicated phase of a split: sub-engine 0 alone
+    if (e_.size() == 1 || (!split_mode_ && e_[0]->split_pending())) {  // rank split: sub-engine 0 alone
       e_[0]->set_progress_hook(hook_);
       struct Unhook {
         IEngine* e;
@@ -334,6 +361,10 @@ class MultiEngine final : public IEngine {
   // largest pool, device to device through the staging buffer.
   void rebalance() {
     const size_t K = e_.size();
+    // no hand-over while the sub-engines still hold the same replicated pool
+    if (split_mode_)
+      for (auto* x : e_)
+        if (x->split_pending()) return;
     std::vector<size_t> sz(K);
     for (size_t i = 0; i < K; ++i) sz[i] = e_[i]->size();
     for (size_t r = 0; r < K; ++r) {
@@ -356,6 +387,10 @@ class MultiEngine final : public IEngine {
       sz[r] += got;
     }
   }
+  bool split_mode_ = false;  // the current solve is split between the sub-engines
+  bool arm_ = false;         // a rank split armed for the next begin()
+  int arank_ = 0, aworld_ = 1;
+  size_t amin_ = 0;
   void* stage(size_t bytes) {
     if (bytes <= buf_bytes_) return buf_;
     if (staging_) {

@@ -47,6 +47,10 @@ class EngineOptions:
     # (same-device copies are cheap: far below the cross-GPU thresholds)
     stream_needy: float = 1 / 16
     stream_donor: float = 1 / 4
+    # > 0: each solve is split in the graph between the sub-engines from the start
+    # (every one begins from the same nodes and keeps a disjoint share once the pool
+    # holds stream_split * streams parents): concurrent streams on a small tree
+    stream_split: int = 0
 
 
 def make_multi(model, backend: str, device: int, opts: EngineOptions):
@@ -59,7 +63,8 @@ def make_multi(model, backend: str, device: int, opts: EngineOptions):
     engines = [model.make_engine(backend, device, sub) for _ in range(k)]
     mod = ops.hip() if backend == "gpu" else ops.cpu()
     window = opts.max_parents if backend == "gpu" else opts.cpu_batch
-    return mod.make_multi_engine(engines, max(1, int(window * opts.stream_needy)), max(2, int(window * opts.stream_donor)))
+    return mod.make_multi_engine(engines, max(1, int(window * opts.stream_needy)), max(2, int(window * opts.stream_donor)),
+                                 split_min=max(0, int(opts.stream_split)))
 
 
 class PfspModel:
