@@ -49,7 +49,9 @@ class EngineOptions:
     stream_donor: float = 1 / 4
     # > 0: each solve is split in the graph between the sub-engines from the start
     # (every one begins from the same nodes and keeps a disjoint share once the pool
-    # holds stream_split * streams parents): concurrent streams on a small tree
+    # holds stream_split * streams parents). Measured on the ta014 headline: 0.224 ms
+    # with one engine, 0.30 / 0.39 ms split over 2 / 3 streams (a latency-bound tree
+    # gains nothing from concurrent streams; profiles/r3/probes/headline_streams_split_ab.txt)
     stream_split: int = 0
 
 
