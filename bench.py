@@ -13,7 +13,9 @@ job (all ranks cooperating, same runtime), unless --no-extras:
   * ta021 (20x20) LB1_d, one complete solve: makespan 2297 and the -u 1 tree
     (260,069,628,524 nodes, sol 14,963,858 — deterministic at every N) are checked;
   * ta056 (50x20) LB2, a fixed time box (--box-s, default 10 s): explored nodes/s
-    (the tree is ~4.6e19 nodes, profiles/r2/ta056_projection.md: no complete solve).
+    (the tree is ~4.6e19 nodes, profiles/r2/ta056_projection.md: no complete solve);
+  * N-Queens N=17 (g=1), best of 3 complete solves: tree 8,017,021,931 and 95,815,104
+    solutions checked (the BASELINE single-GPU N-Queens config; all ranks cooperate).
 They become fields of the same single JSON line ("extras"). An extra that fails is
 reported there (and on stderr) and the headline line is still printed; a watchdog
 (--extras-timeout) prints the line and ends every rank if an extra hangs.
@@ -94,12 +96,13 @@ def main() -> int:
                     help="process group for node transfers (gloo: ranks may share one GPU, for tests)")
     ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default LOCAL_RANK)")
     ap.add_argument("--no-extras", action="store_true", help="headline only (no ta021 / ta056 runs)")
-    ap.add_argument("--extras", default="ta021,ta056", help="comma list of extras to run")
+    ap.add_argument("--extras", default="ta021,ta056,nq17", help="comma list of extras to run")
     ap.add_argument("--box-s", type=float, default=10.0, help="ta056 LB2 time box (seconds)")
     ap.add_argument("--extras-timeout", type=float, default=900.0,
                     help="watchdog: print the line and end every rank after this many seconds of extras")
     ap.add_argument("--extra-inst-lb1d", type=int, default=21, help=argparse.SUPPRESS)
     ap.add_argument("--extra-inst-lb2", type=int, default=56, help=argparse.SUPPRESS)
+    ap.add_argument("--extra-queens-n", type=int, default=17, help=argparse.SUPPRESS)
     ap.add_argument("--extra-ring-gb", type=float, default=64.0)
     ap.add_argument("--extra-streams", type=int, default=3,
                     help="engines per GPU for the extras (csrc/core/multi_engine.hpp; 1 = one engine)")
@@ -217,6 +220,8 @@ def main() -> int:
                     extras[name] = run_solve_extra(a, comm, device, a.extra_inst_lb1d, 0, time_limit=0.0)
                 elif name == "ta056":
                     extras[name] = run_solve_extra(a, comm, device, a.extra_inst_lb2, 2, time_limit=a.box_s)
+                elif name == "nq17":
+                    extras[name] = run_queens_extra(a, comm, device, a.extra_queens_n)
                 else:
                     extras[name] = {"error": "unknown extra"}
                 mine_ok = 1
@@ -230,6 +235,44 @@ def main() -> int:
     out.emit(rec)
     comm.close()
     return 0
+
+
+QUEENS_GOLDEN = {17: (8017021931, 95815104), 16: (1141190302, 14772512), 12: (856188, 14200), 11: (166925, 2680)}
+QUEENS_REF_S = {17: 807.0}  # reference nqueens_c.out -N 17, sequential
+
+
+def run_queens_extra(a, comm, device: int, N: int) -> dict:
+    """N-Queens N (g=1): best of 3 cooperative solves with the headline's runtime."""
+    from dist_gpu_accelerated_tree_search_amd.models.nqueens import QueensModel
+    from dist_gpu_accelerated_tree_search_amd.models.pfsp import EngineOptions
+    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig, DistSolver
+
+    model = QueensModel(N, 1)
+    opts = EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30) if a.backend == "gpu" else EngineOptions()
+    t_setup = time.perf_counter()
+    engine = model.make_engine(a.backend, device, opts)
+    solver = DistSolver(model, engine, comm, DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws),
+                        window=opts.max_parents)
+    t_setup = time.perf_counter() - t_setup
+    best_dt, r = None, None
+    for _ in range(3):
+        comm.barrier()
+        t0 = time.perf_counter()
+        raw = solver.solve_raw(1)
+        comm.barrier()
+        dt = float(comm.allgather_f64([time.perf_counter() - t0]).max())
+        r = solver.result(*raw)
+        best_dt = dt if best_dt is None else min(best_dt, dt)
+    gold = QUEENS_GOLDEN.get(N)
+    d = {"config": f"N-Queens N={N} g=1", "n_gpus": comm.world, "seconds": best_dt, "tree": r.tree, "sol": r.sol,
+         "nodes_per_s": r.tree / best_dt, "engine_setup_s": t_setup, "golden_ok": gold is None or (r.tree, r.sol) == gold}
+    if N in QUEENS_REF_S:
+        d["ref_seconds_seq"] = QUEENS_REF_S[N]
+        d["speedup_vs_ref"] = QUEENS_REF_S[N] / best_dt
+    if not d["golden_ok"]:
+        raise RuntimeError(f"N-Queens N={N}: (tree, sol) {(r.tree, r.sol)} != golden {gold}")
+    del solver, engine
+    return d
 
 
 def run_solve_extra(a, comm, device: int, inst: int, lb: int, time_limit: float) -> dict:

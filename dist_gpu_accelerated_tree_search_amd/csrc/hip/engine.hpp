@@ -198,6 +198,7 @@ class DeviceEngine final : public IEngine {
   }
   std::vector<double> trace() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    flush_load();
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
     TTS_HIP_CHECK(hipStreamSynchronize(xfer_));
     std::vector<double> out;
@@ -216,6 +217,7 @@ class DeviceEngine final : public IEngine {
   void record_event(uintptr_t ev) override {
     if (!ev) return;
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    flush_load();
     TTS_HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(ev), stream_));
   }
   void wait_event(uintptr_t ev) override {
@@ -225,6 +227,7 @@ class DeviceEngine final : public IEngine {
   }
   void fence() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    flush_load();
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
     TTS_HIP_CHECK(hipStreamSynchronize(xfer_));
   }
@@ -491,13 +494,12 @@ class DeviceEngine final : public IEngine {
       std::memcpy(h_begin_, h_ctl_, sizeof(dev::PoolCtl));
       Node* stage = reinterpret_cast<Node*>(reinterpret_cast<char*>(h_begin_) + kUpBytes);
       std::memcpy(stage, nodes, n * sizeof(Node));
-      const int blocks = static_cast<int>(std::min<size_t>(64, (n * (sizeof(Node) / 16) + dev::kBlock - 1) / dev::kBlock + 1));
-      hipLaunchKernelGGL(dev::pool_load_kernel<Node>, dim3(blocks), dim3(dev::kBlock), 0, stream_,
-                         reinterpret_cast<const uint32_t*>(d_begin_), d_ctl_,
-                         reinterpret_cast<const uint4*>(reinterpret_cast<char*>(d_begin_) + kUpBytes), d_ring_,
-                         static_cast<dev::u64>(n));
-      TTS_HIP_CHECK(hipGetLastError());
+      // deferred: the learned first replay starts with the load (one graph launch per
+      // solve); any other device operation launches it first (flush_load)
+      load_n_ = n;
+      load_deferred_ = true;
       loader_pending_ = true;
+      if (!defer_load_) flush_load();
     } else {
       ring_write_top(static_cast<const Node*>(nodes), n, hipMemcpyHostToDevice);
       upload_ctl();  // records up_done_ after both copies
@@ -631,6 +633,7 @@ class DeviceEngine final : public IEngine {
   }
   void synchronize() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    flush_load();
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
   }
 
@@ -702,6 +705,7 @@ class DeviceEngine final : public IEngine {
   // Asynchronous upload of the host shadow (through its own pinned staging copy,
   // so the shadow can be edited again immediately).
   void upload_ctl() {
+    flush_load();
     TTS_HIP_CHECK(hipEventSynchronize(up_done_));
     std::memcpy(h_up_, h_ctl_, sizeof(dev::PoolCtl));
     TTS_HIP_CHECK(hipMemcpyAsync(d_ctl_, h_up_, sizeof(dev::PoolCtl), hipMemcpyHostToDevice, stream_));
@@ -711,6 +715,7 @@ class DeviceEngine final : public IEngine {
   // Host shadow must be current (sync_ctl); between graph replays slot 0 is active
   // and the latest children are in buffer phase_ & 1 (graphs of 3k iterations).
   void normalize() {
+    flush_load();
     // subtrees finished inside iterations (N-Queens)
     for (auto& x : h_ctl_->xacc) {
       h_ctl_->tree += x.tree;
@@ -773,6 +778,7 @@ class DeviceEngine final : public IEngine {
   }
   // Host shadow current and every asynchronous spill copy folded in.
   void settle() {
+    flush_load();
     sync_ctl();
     commit_spill_ahead();
     if (refill_n_) finish_refill();
@@ -799,6 +805,7 @@ class DeviceEngine final : public IEngine {
   // Asynchronous D2H of the n oldest ring nodes into the pinned spill, on the
   // transfer stream; the ring span stays reserved until the copy has completed.
   void spill_bottom(size_t n) {
+    flush_load();
     n = std::min(n, dev_stack());
     if (n == 0) return;
     order(stream_, xfer_);  // the nodes were written by earlier replays
@@ -857,6 +864,7 @@ class DeviceEngine final : public IEngine {
   // pool when the copy has completed (fold_refill). Returns false without room.
   bool start_refill(size_t want) {
     if (refill_n_ || spill_.empty() || want == 0) return false;
+    flush_load();
     // like push_host: the device part stays within half the ring, and the smallest
     // graph must still fit afterwards (else refills and spills would alternate)
     const size_t used = dev_total() + reserved_;
@@ -898,9 +906,12 @@ class DeviceEngine final : public IEngine {
     const int m = next_mirror_;
     next_mirror_ ^= 1;
     const int k = K > 0 ? K : ks_[gi];
+    const bool with_load = load_deferred_ && K > 0 && cfg_.use_graphs;
+    if (!with_load) flush_load();
     const hipEvent_t tr = trace_ ? trace_mark(stream_) : nullptr;
     if (cfg_.use_graphs) {
-      hipGraphExec_t g = K > 0 ? first_graph(K)[m] : graphs_[phase_ / 3][m][gi];
+      hipGraphExec_t g = K > 0 ? first_graph(K, with_load)[m] : graphs_[phase_ / 3][m][gi];
+      load_deferred_ = false;
       if (tr) TTS_HIP_CHECK(hipEventRecord(tr, stream_));  // after a first-use capture's sync
       TTS_HIP_CHECK(hipGraphLaunch(g, stream_));
     } else {
@@ -917,15 +928,37 @@ class DeviceEngine final : public IEngine {
     ++stats_.launches;
     fresh_ = false;
   }
-  // The learned first replay (phase 0, both mirrors), captured on first use.
-  const std::array<hipGraphExec_t, 2>& first_graph(int K) {
-    auto it = first_graphs_.find(K);
+  // The learned first replay (phase 0, both mirrors), captured on first use; with_load:
+  // the graph starts with begin()'s deferred load (pool_load_staged_kernel).
+  const std::array<hipGraphExec_t, 2>& first_graph(int K, bool with_load) {
+    const int key = with_load ? -K : K;
+    auto it = first_graphs_.find(key);
     if (it == first_graphs_.end()) {
       TTS_HIP_CHECK(hipStreamSynchronize(stream_));
-      std::array<hipGraphExec_t, 2> g{capture(K, 0, 0), capture(K, 1, 0)};
-      it = first_graphs_.emplace(K, g).first;
+      std::array<hipGraphExec_t, 2> g{capture(K, 0, 0, with_load), capture(K, 1, 0, with_load)};
+      it = first_graphs_.emplace(key, g).first;
     }
     return it->second;
+  }
+  // begin()'s load kernel, unless a graph replay already started with it
+  void launch_load(hipStream_t s, bool staged) {
+    const int blocks = static_cast<int>(
+        std::min<size_t>(64, (std::max<size_t>(load_n_, kStageNodes * !!staged) * (sizeof(Node) / 16) + dev::kBlock - 1) /
+                                     dev::kBlock + 1));
+    const uint32_t* sc = reinterpret_cast<const uint32_t*>(d_begin_);
+    const uint4* sn = reinterpret_cast<const uint4*>(reinterpret_cast<char*>(d_begin_) + kUpBytes);
+    if (staged)
+      hipLaunchKernelGGL(dev::pool_load_staged_kernel<Node>, dim3(blocks), dim3(dev::kBlock), 0, s, sc, d_ctl_, sn,
+                         d_ring_);
+    else
+      hipLaunchKernelGGL(dev::pool_load_kernel<Node>, dim3(blocks), dim3(dev::kBlock), 0, s, sc, d_ctl_, sn, d_ring_,
+                         static_cast<dev::u64>(load_n_));
+    TTS_HIP_CHECK(hipGetLastError());
+  }
+  void flush_load() {
+    if (!load_deferred_) return;
+    load_deferred_ = false;
+    launch_load(stream_, false);
   }
   void push_inflight(int m, int k) {
     inflight_.push_back(m);
@@ -933,11 +966,12 @@ class DeviceEngine final : public IEngine {
     inflight_seq_.push_back(++launched_seq_);
   }
 
-  hipGraphExec_t capture(int K, int mirror, int phase) {
+  hipGraphExec_t capture(int K, int mirror, int phase, bool with_load = false) {
     hipStream_t cs;
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     hipGraph_t g;
     TTS_HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    if (with_load) launch_load(cs, true);
     for (int i = 0; i < K; ++i) Traits::launch(args_, (phase + i) % 6, grid_, cs);
     auto pa = args_.pool;
     pa.mirror = d_mirror_[mirror];
@@ -964,6 +998,12 @@ class DeviceEngine final : public IEngine {
   dev::PoolCtl* h_begin_ = nullptr;  // begin()'s mapped staging (control block + nodes), read by pool_load_kernel
   dev::PoolCtl* d_begin_ = nullptr;  // ... its device address
   bool loader_pending_ = false;      // a load kernel may still read h_begin_
+  bool load_deferred_ = false;       // begin()'s load not launched yet (see launch_graph / flush_load)
+  bool defer_load_ = [] {            // TTS_DEFER_LOAD=0: launch it in begin() (A/B runs)
+    const char* f = std::getenv("TTS_DEFER_LOAD");
+    return !(f && f[0] == '0');
+  }();
+  size_t load_n_ = 0;
   static constexpr size_t kUpBytes = (sizeof(dev::PoolCtl) + 255) & ~size_t(255);
   static constexpr size_t kStageNodes = 4096;
   dev::PoolCtl* h_mirror_[2] = {nullptr, nullptr};

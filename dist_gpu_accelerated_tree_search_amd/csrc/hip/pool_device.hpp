@@ -344,8 +344,8 @@ __global__ __launch_bounds__(kBlock) void pool_flatten_kernel(PoolArgs<Node> pa,
 // (each a blit dispatch plus its API call) ahead of the first graph replay. The nodes
 // go to ring[0..n) (begin() resets the ring base).
 template <class Node>
-__global__ __launch_bounds__(kBlock) void pool_load_kernel(const uint32_t* __restrict__ src_ctl, PoolCtl* dctl,
-                                                           const uint4* __restrict__ src_nodes, Node* ring, u64 n) {
+__device__ inline void pool_load_body(const uint32_t* __restrict__ src_ctl, PoolCtl* dctl,
+                                      const uint4* __restrict__ src_nodes, Node* ring, u64 n) {
   constexpr int VPN = sizeof(Node) / 16;
   constexpr int W = static_cast<int>(sizeof(PoolCtl) / 4);
   const u64 stride = static_cast<u64>(gridDim.x) * kBlock;
@@ -354,6 +354,21 @@ __global__ __launch_bounds__(kBlock) void pool_load_kernel(const uint32_t* __res
   for (u64 i = tid; i < static_cast<u64>(W); i += stride) d[i] = src_ctl[i];
   uint4* dn = reinterpret_cast<uint4*>(ring);
   for (u64 x = tid; x < n * VPN; x += stride) dn[x] = src_nodes[x];
+}
+template <class Node>
+__global__ __launch_bounds__(kBlock) void pool_load_kernel(const uint32_t* __restrict__ src_ctl, PoolCtl* dctl,
+                                                           const uint4* __restrict__ src_nodes, Node* ring, u64 n) {
+  pool_load_body<Node>(src_ctl, dctl, src_nodes, ring, n);
+}
+
+// The same load with the node count read from the staged control block (slot 0's
+// stack): a kernel node of a captured graph (the learned first replay starts with it,
+// so a solve is one graph launch; DeviceEngine::begin defers its load to that graph).
+template <class Node>
+__global__ __launch_bounds__(kBlock) void pool_load_staged_kernel(const uint32_t* __restrict__ src_ctl, PoolCtl* dctl,
+                                                                  const uint4* __restrict__ src_nodes, Node* ring) {
+  const u64 n = reinterpret_cast<const PoolCtl*>(src_ctl)->slot[0].stack;  // uniform: one scalar load per wave
+  pool_load_body<Node>(src_ctl, dctl, src_nodes, ring, n);
 }
 
 // Rank share of a replicated pool: out[t] = ring[bot + rank + t*world], t < keep

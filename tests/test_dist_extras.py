@@ -91,12 +91,12 @@ def test_checkpoint_rejects_mixed_rounds(tmp_path):
 
 def test_bench_extras_cpu_gloo():
     # the driver's launch line with 2 ranks (CPU engines, gloo): one JSON line with the
-    # headline and both extras; small stand-ins keep it short (ta014 for the complete
-    # LB1_d solve, a 0.5-s ta056 LB2 box)
+    # headline and the extras; small stand-ins keep it short (ta014 for the complete
+    # LB1_d solve, a 0.5-s ta056 LB2 box, N-Queens N=11 for N=17)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
            "--steps", "1", "--warmup", "0", "--backend", "cpu", "--comm", "gloo", "--extra-inst-lb1d", "14",
-           "--box-s", "0.5"]
+           "--box-s", "0.5", "--extra-queens-n", "11"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
@@ -108,6 +108,7 @@ def test_bench_extras_cpu_gloo():
     assert ex["ta021"]["complete"] is True
     assert ex["ta056"]["complete"] is False and ex["ta056"]["nodes_per_s"] > 0
     assert ex["ta056"]["time_box_s"] == 0.5
+    assert (ex["nq17"]["tree"], ex["nq17"]["sol"]) == (166925, 2680) and ex["nq17"]["golden_ok"] is True
 
 
 def test_bench_runs_without_transfers_after_failed_preflight():

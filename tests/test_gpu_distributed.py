@@ -98,6 +98,21 @@ def test_gpu_multi_engine_golden(key, streams):
         assert (r.tree, r.sol, r.best) == gold
 
 
+@pytest.mark.parametrize("key,streams", [((14, 1), 2), ((8, 0), 3)])
+def test_gpu_multi_engine_split_golden(key, streams):
+    # stream_split: the solve is split in the graph between the sub-engines (same begin
+    # nodes, disjoint shares after the replicated prefix, two-level iterations included)
+    from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel
+    from dist_gpu_accelerated_tree_search_amd.search import solve_engine
+
+    gold = {(14, 1): (2573652, 2648, 1377), (8, 0): (113458723, 808498, 1206)}[key]
+    model = PfspModel(*key)
+    eng = model.make_engine("gpu", 0, EngineOptions(streams=streams, stream_split=512, ring_bytes=3 << 30))
+    for _ in range(2):
+        r = solve_engine(model, eng)
+        assert (r.tree, r.sol, r.best) == gold
+
+
 def test_gpu_multi_engine_queens():
     from dist_gpu_accelerated_tree_search_amd import EngineOptions, QueensModel
     from dist_gpu_accelerated_tree_search_amd.search import solve_engine
