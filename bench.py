@@ -248,7 +248,10 @@ def run_queens_extra(a, comm, device: int, N: int) -> dict:
     from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig, DistSolver
 
     model = QueensModel(N, 1)
-    opts = EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30) if a.backend == "gpu" else EngineOptions()
+    # two engines per GPU with the solve split between them in the graph: N=17 74 -> 48 ms
+    # on one MI355X (profiles/r3/queens/streams_probe.txt)
+    opts = EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30, streams=2, stream_split=512) \
+        if a.backend == "gpu" else EngineOptions(streams=2, stream_split=8)
     t_setup = time.perf_counter()
     engine = model.make_engine(a.backend, device, opts)
     solver = DistSolver(model, engine, comm, DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws),
@@ -265,7 +268,8 @@ def run_queens_extra(a, comm, device: int, N: int) -> dict:
         best_dt = dt if best_dt is None else min(best_dt, dt)
     gold = QUEENS_GOLDEN.get(N)
     d = {"config": f"N-Queens N={N} g=1", "n_gpus": comm.world, "seconds": best_dt, "tree": r.tree, "sol": r.sol,
-         "nodes_per_s": r.tree / best_dt, "engine_setup_s": t_setup, "golden_ok": gold is None or (r.tree, r.sol) == gold}
+         "nodes_per_s": r.tree / best_dt, "engine_setup_s": t_setup, "engines_per_gpu": opts.streams,
+         "golden_ok": gold is None or (r.tree, r.sol) == gold}
     if N in QUEENS_REF_S:
         d["ref_seconds_seq"] = QUEENS_REF_S[N]
         d["speedup_vs_ref"] = QUEENS_REF_S[N] / best_dt

@@ -55,8 +55,10 @@ def run_one(name: str, gpus: int) -> dict:
     else:
         # (N-Queens: the pool stays far below 8 GB with subtree finishing; the ring is
         # allocated inside the timed region, like the reference's setup)
-        opts = EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30) if c["problem"] == "queens" else \
-            EngineOptions(ring_bytes=64 << 30)
+        # (two engines with the solve split between them for N-Queens; three sharing
+        # engines for the large PFSP trees: profiles/r3/queens, profiles/r3/streams_probe.txt)
+        opts = EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30, streams=2, stream_split=512) \
+            if c["problem"] == "queens" else EngineOptions(ring_bytes=64 << 30, streams=3)
         r = solve_gpu(model, opts=opts)
         n = 1
     dt = time.perf_counter() - t0

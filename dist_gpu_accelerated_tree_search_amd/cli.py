@@ -246,6 +246,10 @@ def nqueens_main(argv: list[str]) -> int:
     ap.add_argument("-M", type=int, default=50000)
     ap.add_argument("-D", type=int, default=1)
     ap.add_argument("--max-parents", type=int, default=1 << 20)
+    # engines per GPU, the solve split in the graph between them: N=17 74 -> 48 ms on one
+    # MI355X with 2 (profiles/r3/queens/streams_probe.txt)
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--stream-split", type=int, default=512)
     a = ap.parse_args(argv)
     for name, v in (("N", a.N), ("g", a.g), ("m", a.m)):
         if v < 1:
@@ -267,14 +271,17 @@ def nqueens_main(argv: list[str]) -> int:
         return 0
     if a.D == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         print(report.queens_settings(a.N, a.g, "Single-GPU C++/HIP (MI355X)"))
-        eng = model.make_engine("gpu", 0, EngineOptions(max_parents=a.max_parents))
+        eng = model.make_engine("gpu", 0, EngineOptions(max_parents=a.max_parents, streams=max(1, a.streams),
+                                                        stream_split=a.stream_split if a.streams > 1 else 0))
         r = solve_engine(model, eng, m=a.m, verbose=True)
         print(report.queens_results(r.tree, r.sol, r.elapsed))
         return 0
     from .parallel.workers import solve_rank
 
     spec = {"problem": "nqueens", "N": a.N, "G": a.g, "backend": "gpu",
-            "engine": {"max_parents": a.max_parents}, "dist": {"m": a.m, "init_per_rank": a.m}}
+            "engine": {"max_parents": a.max_parents, "streams": max(1, a.streams),
+                       "stream_split": a.stream_split if a.streams > 1 else 0},
+            "dist": {"m": a.m, "init_per_rank": a.m}}
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         res = solve_rank(spec)
         if res["rank"] != 0:
