@@ -113,14 +113,18 @@ def test_gpu_multi_engine_split_golden(key, streams):
         assert (r.tree, r.sol, r.best) == gold
 
 
-def test_gpu_multi_engine_queens():
+@pytest.mark.parametrize("split", [0, 512])
+def test_gpu_multi_engine_queens(split):
+    # (split 512: the default N-Queens configuration of the CLI and bench.py)
     from dist_gpu_accelerated_tree_search_amd import EngineOptions, QueensModel
     from dist_gpu_accelerated_tree_search_amd.search import solve_engine
 
     model = QueensModel(13, 1)
-    eng = model.make_engine("gpu", 0, EngineOptions(streams=2, ring_bytes=1 << 29, max_parents=1 << 14))
-    r = solve_engine(model, eng)
-    assert (r.tree, r.sol) == (4674889, 73712)
+    eng = model.make_engine("gpu", 0, EngineOptions(streams=2, stream_split=split, ring_bytes=1 << 29,
+                                                    max_parents=1 << 14))
+    for _ in range(2):
+        r = solve_engine(model, eng)
+        assert (r.tree, r.sol) == (4674889, 73712)
 
 
 def test_gpu_multi_engine_ranks():
