@@ -492,7 +492,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK == 5
 void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
     pfsp_expand_lb2<NJ, M>(a, t);
-  else if constexpr (LBK == 5 && NJ <= 64)
+  else if constexpr (LBK == 5 && NJ <= 128)
     pfsp_expand_lb2<NJ, M, true>(a, t);  // two children per lane, packed u16 walks
   else if constexpr (LBK == 5)
     pfsp_expand_lb2<NJ, M>(a, t);  // (job sets of one word only)
@@ -631,19 +631,31 @@ __device__ inline void lb2_walk_pipe(const uint4* rq, int ndouble, const u64 (&m
 // halves (v_pk_add_u16 / v_pk_max_u16, the record fields broadcast by op_sel); each
 // half skips the jobs of its own child's scheduled set (bit field insert on a
 // per-half keep mask). Exact as long as every value of the walk fits 16 bits: a walk
-// value is a path length through the p matrix, at most the sum of all processing
-// times (host check lb2_pk_ok: < 65536).
+// value is a path length through the p matrix (host check lb2_pk_ok: (jobs + machines
+// - 1) x max p < 65536). Job sets of NW > 1 words (100-job instances) pick the word
+// of the record's job first (one 64-bit select per word and child).
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 __device__ inline uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
-__device__ inline void lb2_step2(uint32_t x, uint32_t y, u64 ma, u64 mb, uint32_t& t0, uint32_t& t1) {
+template <int NW>
+__device__ inline void lb2_step2(uint32_t x, uint32_t y, const u64 (&mav)[NW], const u64 (&mbv)[NW], uint32_t& t0,
+                                 uint32_t& t1) {
   const u16x2 p0 = static_cast<u16x2>(static_cast<unsigned short>(x >> 16));
   const u16x2 lag = static_cast<u16x2>(static_cast<unsigned short>(y >> 16));
   const u16x2 p1 = static_cast<u16x2>(static_cast<unsigned short>(y & 0xffff));
   const u16x2 n0 = as_u16x2(t0) + p0;
   const u16x2 n1 = __builtin_elementwise_max(as_u16x2(t1), n0 + lag) + p1;
   const uint32_t job = x & 63u;
+  u64 ma = mav[0], mb = mbv[0];
+  if constexpr (NW > 1) {
+    const uint32_t wj = (x & 0xffffu) >> 6;
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      ma = wj == static_cast<uint32_t>(w) ? mav[w] : ma;
+      mb = wj == static_cast<uint32_t>(w) ? mbv[w] : mb;
+    }
+  }
   // all ones where the half's child skips the job: v_lshrrev_b64 + v_bfe_i32 per child
   // (spelled with the intrinsics: the plain (m >> job) & 1 becomes a mask-and-compare
   // sequence twice as long), halves merged by one v_perm_b32
@@ -654,20 +666,22 @@ __device__ inline void lb2_step2(uint32_t x, uint32_t y, u64 ma, u64 mb, uint32_
   t1 = (t1 & keep) | (as_u32(n1) & ~keep);
 }
 
-__device__ inline void lb2_walk_pipe2(const uint4* rq, int ndouble, u64 ma, u64 mb, uint32_t& t0, uint32_t& t1) {
+template <int NW>
+__device__ inline void lb2_walk_pipe2(const uint4* rq, int ndouble, const u64 (&ma)[NW], const u64 (&mb)[NW],
+                                      uint32_t& t0, uint32_t& t1) {
   uint4 a0 = rq[0], a1 = rq[1], b0 = rq[2], b1 = rq[3];
   for (int g = 0; g < ndouble; ++g) {
-    lb2_step2(a0.x, a0.y, ma, mb, t0, t1);
-    lb2_step2(a0.z, a0.w, ma, mb, t0, t1);
-    lb2_step2(a1.x, a1.y, ma, mb, t0, t1);
-    lb2_step2(a1.z, a1.w, ma, mb, t0, t1);
+    lb2_step2<NW>(a0.x, a0.y, ma, mb, t0, t1);
+    lb2_step2<NW>(a0.z, a0.w, ma, mb, t0, t1);
+    lb2_step2<NW>(a1.x, a1.y, ma, mb, t0, t1);
+    lb2_step2<NW>(a1.z, a1.w, ma, mb, t0, t1);
     a0 = rq[4 * g + 4];
     a1 = rq[4 * g + 5];
     __builtin_amdgcn_sched_barrier(0);
-    lb2_step2(b0.x, b0.y, ma, mb, t0, t1);
-    lb2_step2(b0.z, b0.w, ma, mb, t0, t1);
-    lb2_step2(b1.x, b1.y, ma, mb, t0, t1);
-    lb2_step2(b1.z, b1.w, ma, mb, t0, t1);
+    lb2_step2<NW>(b0.x, b0.y, ma, mb, t0, t1);
+    lb2_step2<NW>(b0.z, b0.w, ma, mb, t0, t1);
+    lb2_step2<NW>(b1.x, b1.y, ma, mb, t0, t1);
+    lb2_step2<NW>(b1.z, b1.w, ma, mb, t0, t1);
     b0 = rq[4 * g + 6];
     b1 = rq[4 * g + 7];
     __builtin_amdgcn_sched_barrier(0);
@@ -808,7 +822,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         const int nq = min(P - q0, R);
         if constexpr (PK) {
           // tasks (pair, child pair): children alist[2k], alist[2k + 1] share a lane
-          static_assert(G::NW == 1, "packed walks: job sets of one word");
+          static_assert(G::NW <= 2, "packed walks: job sets of at most two words");
           const int nk = (na + 1) >> 1;
           int qq = tid / nk, kk = tid - (tid / nk) * nk;
           const int dq = kBlock / nk, dk = kBlock - dq * nk;
@@ -822,7 +836,12 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
               const int cbb = cb >= 0 ? cb : ca;
               uint32_t t0 = static_cast<uint32_t>(sm.cf[m0][ca]) | (static_cast<uint32_t>(sm.cf[m0][cbb]) << 16);
               uint32_t t1 = static_cast<uint32_t>(sm.cf[m1][ca]) | (static_cast<uint32_t>(sm.cf[m1][cbb]) << 16);
-              const u64 ma = sm.cm[ca][0], mb = cb >= 0 ? sm.cm[cbb][0] : ~0ull;
+              u64 ma[G::NW], mb[G::NW];
+#pragma unroll
+              for (int w = 0; w < G::NW; ++w) {
+                ma[w] = sm.cm[ca][w];
+                mb[w] = cb >= 0 ? sm.cm[cbb][w] : ~0ull;
+              }
               lb2_walk_pipe2(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, ma, mb, t0, t1);
               const int tl0 = static_cast<int>(pi.y & 0xffff), tl1 = static_cast<int>(pi.y >> 16);
               if (la)

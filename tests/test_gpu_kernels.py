@@ -76,7 +76,7 @@ def test_lb2_expand_path_matches_cpu(inst, best_from, variant):
     # B3 decision) against cpu_lb2 child by child: exact values when best = INT_MAX,
     # the lb < best decision otherwise
     model = PfspModel(inst, 2)
-    if variant == 4 and (model.jobs > 64 or (model.jobs + model.machines - 1) * max(model.native.p) >= 65536):
+    if variant == 4 and (model.jobs > 128 or (model.jobs + model.machines - 1) * max(model.native.p) >= 65536):
         pytest.skip("packed walks need job sets of one word and 16-bit walk values (lb2_pk_ok)")
     n = {20: 600, 50: 200, 100: 40}.get(model.jobs, 12)
     nodes = random_nodes(model.jobs, n, inst * 7 + variant)
