@@ -111,6 +111,21 @@ def test_bench_extras_cpu_gloo():
     assert (ex["nq17"]["tree"], ex["nq17"]["sol"]) == (166925, 2680) and ex["nq17"]["golden_ok"] is True
 
 
+def test_bench_four_ranks_cpu_gloo():
+    # the driver's N=4 launch line shape (4 ranks, one JSON line from rank 0, golden tree,
+    # per-rank work shares), CPU engines
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "4",
+           "--steps", "2", "--warmup", "1", "--backend", "cpu", "--comm", "gloo", "--no-extras"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 4 and rec["steps"] == 2 and rec["config"]["parallelism"] == "dp4+ws"
+    assert (rec["config"]["tree"], rec["config"]["sol"], rec["config"]["makespan"]) == GOLD
+
+
 def test_bench_runs_without_transfers_after_failed_preflight():
     # a rank whose point-to-point check fails (fault injection): bench.py reports it in
     # the JSON line and measures the headline without work sharing (static split), golden
