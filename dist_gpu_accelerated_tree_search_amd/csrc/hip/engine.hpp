@@ -26,7 +26,6 @@
 #include <cstring>
 #include <deque>
 #include <memory>
-#include <type_traits>
 #include <vector>
 
 #include "../core/engine_api.hpp"
@@ -42,13 +41,6 @@ namespace tts {
 //   static void flatten(const dev::PoolArgs<Node>&, int grid, hipStream_t);
 //   static void finalize(const dev::PoolArgs<Node>&, hipStream_t);
 //   static int blocks_per_cu();
-//   optional: static void launch_fin(const Args&, int t, int b, int grid, hipStream_t) —
-//   iteration t with the finalize of buffer b fused into its last workgroup
-template <class T, class = void>
-struct HasFusedFinalize : std::false_type {};
-template <class T>
-struct HasFusedFinalize<T, std::void_t<decltype(&T::launch_fin)>> : std::true_type {};
-
 template <class Traits>
 class DeviceEngine final : public IEngine {
  public:
@@ -542,7 +534,9 @@ class DeviceEngine final : public IEngine {
       a.pool.max_chunks = static_cast<int>((win + Traits::kParentsPerChunk - 1) / Traits::kParentsPerChunk);
       const int m = next_mirror_;
       next_mirror_ ^= 1;
-      enqueue_iters(a, 0, 6, m, stream_);
+      for (int i = 0; i < 6; ++i) Traits::launch(a, i, grid_, stream_);
+      a.pool.mirror = d_mirror_[m];
+      Traits::finalize(a.pool, 0, stream_);
       TTS_HIP_CHECK(hipGetLastError());
       TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
       push_inflight(m, 6);
@@ -921,7 +915,10 @@ class DeviceEngine final : public IEngine {
       if (tr) TTS_HIP_CHECK(hipEventRecord(tr, stream_));  // after a first-use capture's sync
       TTS_HIP_CHECK(hipGraphLaunch(g, stream_));
     } else {
-      enqueue_iters(args_, phase_, k, m, stream_);
+      for (int i = 0; i < k; ++i) Traits::launch(args_, (phase_ + i) % 6, grid_, stream_);
+      auto pa = args_.pool;
+      pa.mirror = d_mirror_[m];
+      Traits::finalize(pa, ((phase_ + k) % 6) & 1, stream_);
       TTS_HIP_CHECK(hipGetLastError());
     }
     TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
@@ -963,21 +960,6 @@ class DeviceEngine final : public IEngine {
     load_deferred_ = false;
     launch_load(stream_, false);
   }
-  // k iterations from phase, then the finalize into mirror m (fused into the last
-  // iteration's kernel where the kernel has it: one graph node less per replay)
-  void enqueue_iters(Args a, int phase, int k, int m, hipStream_t s) {
-    a.pool.mirror = d_mirror_[m];
-    const int b = ((phase + k) % 6) & 1;
-    if constexpr (HasFusedFinalize<Traits>::value) {
-      if (fused_fin_ && k > 0) {
-        for (int i = 0; i < k - 1; ++i) Traits::launch(a, (phase + i) % 6, grid_, s);
-        Traits::launch_fin(a, (phase + k - 1) % 6, b, grid_, s);
-        return;
-      }
-    }
-    for (int i = 0; i < k; ++i) Traits::launch(a, (phase + i) % 6, grid_, s);
-    Traits::finalize(a.pool, b, s);
-  }
   void push_inflight(int m, int k) {
     inflight_.push_back(m);
     inflight_k_.push_back(k);  // iterations of the replay
@@ -990,7 +972,10 @@ class DeviceEngine final : public IEngine {
     hipGraph_t g;
     TTS_HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     if (with_load) launch_load(cs, true);
-    enqueue_iters(args_, phase, K, mirror, cs);
+    for (int i = 0; i < K; ++i) Traits::launch(args_, (phase + i) % 6, grid_, cs);
+    auto pa = args_.pool;
+    pa.mirror = d_mirror_[mirror];
+    Traits::finalize(pa, ((phase + K) % 6) & 1, cs);
     TTS_HIP_CHECK(hipStreamEndCapture(cs, &g));
     hipGraphExec_t exec;
     TTS_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
@@ -1016,10 +1001,6 @@ class DeviceEngine final : public IEngine {
   bool load_deferred_ = false;       // begin()'s load not launched yet (see launch_graph / flush_load)
   bool defer_load_ = [] {            // TTS_DEFER_LOAD=0: launch it in begin() (A/B runs)
     const char* f = std::getenv("TTS_DEFER_LOAD");
-    return !(f && f[0] == '0');
-  }();
-  bool fused_fin_ = [] {             // TTS_FUSED_FIN=0: separate finalize kernel node (A/B runs)
-    const char* f = std::getenv("TTS_FUSED_FIN");
     return !(f && f[0] == '0');
   }();
   size_t load_n_ = 0;

@@ -65,11 +65,7 @@ struct PfspFrontTraits {
   static constexpr int kLocalSteps = G::LT;
   static constexpr int kMaxChunks = G::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, s, a, t, -1);
-  }
-  // a graph's last iteration with the finalize of buffer b fused in (a.pool.mirror set)
-  static void launch_fin(const Args& a, int t, int b, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, s, a, t, b);
+    hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
   }
   static void flatten(const dev::PoolArgs<Node>& pa, int b, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::SLOT, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,

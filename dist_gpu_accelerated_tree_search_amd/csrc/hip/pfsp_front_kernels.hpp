@@ -428,9 +428,11 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
 // (8 waves per SIMD for M <= 10, SGPRs spilled to VGPR lanes, measured: ta014 +2 %,
 // ta008 -4 %; not kept, profiles/r3/probes/front_w8_ab.txt)
 template <int M>
-__device__ __forceinline__ void front_iteration(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, int t) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 10 ? 6 : 4)))
+void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
   using G = FrontGeom<M>;
   using Node = PfspFrontNode<M>;
+  __shared__ FrontSmem<M> sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   // p table loads issued together with pool_begin's (one memory round trip)
@@ -501,15 +503,6 @@ __device__ __forceinline__ void front_iteration(const PfspFrontArgs<M>& a, Front
     }
     front_emit<M>(sm, w, surv, reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off));
   }
-}
-// fin >= 0: the last iteration of a graph, which also runs the finalize (buffer fin)
-// in its last workgroup to finish (pool_finalize_tail)
-template <int M>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 10 ? 6 : 4)))
-void pfsp_front_kernel(PfspFrontArgs<M> a, int t, int fin) {
-  __shared__ FrontSmem<M> sm;
-  front_iteration<M>(a, sm, t);
-  if (fin >= 0) pool_finalize_tail<PfspFrontNode<M>, FrontGeom<M>::MAXCHUNKS>(a.pool, fin, sm.pool);
 }
 
 // Reference-style evaluation for the tests (ref evaluate_gpu, PFSP_gpu_lib.cu:129-152):

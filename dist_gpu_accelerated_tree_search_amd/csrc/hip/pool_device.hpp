@@ -56,7 +56,7 @@ struct PoolCtl {
   // drop the replicated counts gathered so far. Same line as `bot`.
   int split_world;    // <= 1: no split armed
   int split_rank;
-  unsigned fin_count;  // workgroups done with a fused-finalize iteration (pool_finalize_tail); 0 between kernels
+  int pad0;
   u64 split_min;
   // nodes pushed and leaves counted inside subtrees a thread explored to the end (N-Queens
   // finishing: 64-bit counts, one accumulator line per 8th of the grid; the host folds them)
@@ -417,7 +417,8 @@ __global__ __launch_bounds__(kBlock) void pool_weight_kernel(const Node* __restr
 // (b: the buffer the graph's last iteration wrote — graphs of 3k iterations end at phase 0
 // or 3: slot 0 either way, buffer b = phase & 1)
 template <class Node, int MAXCHUNKS>
-__device__ inline void pool_finalize_body(const PoolArgs<Node>& pa, int b, PoolSmem<MAXCHUNKS>& ps) {
+__global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa, int b) {
+  __shared__ PoolSmem<MAXCHUNKS> ps;
   const int n = pa.ctl->slot[0].nch;
   const u64 seq = pa.ctl->seq + 1;
   int c = 0, l = 0, in = 0;
@@ -446,10 +447,9 @@ __device__ inline void pool_finalize_body(const PoolArgs<Node>& pa, int b, PoolS
   constexpr int kSeq = static_cast<int>(offsetof(PoolCtl, seq) / 4);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pa.ctl);
   uint32_t* dst = reinterpret_cast<uint32_t*>(pa.mirror);
-  constexpr int kFin = static_cast<int>(offsetof(PoolCtl, fin_count) / 4);
   for (int i = threadIdx.x; i < static_cast<int>(sizeof(PoolCtl) / 4); i += kBlock) {
     if (i == kSeq || i == kSeq + 1) continue;
-    uint32_t x = i == kFin ? 0u : src[i];
+    uint32_t x = src[i];
     if (i == kPc) x = static_cast<uint32_t>(ct);
     if (i == kPc + 1) x = 0;
     if (i == kPl) x = static_cast<uint32_t>(lt);
@@ -463,35 +463,6 @@ __device__ inline void pool_finalize_body(const PoolArgs<Node>& pa, int b, PoolS
     __threadfence_system();
     __hip_atomic_store(&pa.mirror->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-}
-template <class Node, int MAXCHUNKS>
-__global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa, int b) {
-  __shared__ PoolSmem<MAXCHUNKS> ps;
-  pool_finalize_body<Node, MAXCHUNKS>(pa, b, ps);
-}
-
-// The same finalize fused into a graph's last iteration kernel (kernels that take a
-// `fin` argument): every workgroup counts itself done at its end, and the last one
-// (agent-scope acq_rel on the counter, fences on both sides: the chunk counts of the
-// other workgroups may sit in another XCD's L2) folds the counts and publishes the
-// mirror — one dependent kernel node less per replay. It resets the counter for the
-// next fused kernel; every workgroup of the grid must call this (no early exits).
-template <class Node, int MAXCHUNKS>
-__device__ inline void pool_finalize_tail(const PoolArgs<Node>& pa, int b, PoolSmem<MAXCHUNKS>& ps) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned prev =
-        __hip_atomic_fetch_add(&pa.ctl->fin_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    ps.scan[0] = prev + 1 == gridDim.x;
-  }
-  __syncthreads();
-  const bool last = ps.scan[0] != 0;
-  __syncthreads();  // the flag is read before the scans below reuse ps.scan
-  if (!last) return;
-  __threadfence();
-  if (threadIdx.x == 0) pa.ctl->fin_count = 0;
-  pool_finalize_body<Node, MAXCHUNKS>(pa, b, ps);
 }
 
 }  // namespace dev
