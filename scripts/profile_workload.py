@@ -33,6 +33,14 @@ elif which == "ta056":  # LB2 50x20, time-boxed (the full tree takes far longer)
     st = eng.stats()
     print(which, st["tree"], st["iters"], "pool", eng.size())
     raise SystemExit(0)
+elif which == "ta081":  # LB2 100x20 (two-word job sets), time-boxed
+    m = PfspModel(81, 2); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=32 << 30))
+    nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
+    eng.begin(nodes, int(best))
+    eng.run(max_seconds=1.5)
+    st = eng.stats()
+    print(which, st["tree"], st["iters"], "pool", eng.size())
+    raise SystemExit(0)
 elif which == "ta021":  # LB1_d 20x20 (BASELINE 8-GPU config), time-boxed
     m = PfspModel(21, 0); eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=32 << 30))
     nodes, tree1, sol1, best = m.warmup(m.initial_best(1), 25)
