@@ -204,7 +204,7 @@ def main() -> int:
             extras["error"] = f"watchdog: extras exceeded {a.extras_timeout:.0f} s; every rank exits"
             log(f"rank {comm.rank}: {extras['error']}")
             out.emit(rec)
-            os._exit(0)
+            os._exit(3)  # the line is printed, but a hung extra is a failure
 
         dog = threading.Timer(a.extras_timeout, fire)
         dog.daemon = True

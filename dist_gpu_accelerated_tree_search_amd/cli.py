@@ -101,8 +101,11 @@ def _steal_cap(a) -> int:
 
 
 def _rank_spec(a, world: int = 1) -> dict:
-    # -C 1 under torchrun: a CPU worker thread per rank (ref NB_THREADS_GPU - 1 threads)
-    cpu = max(1, _cpu_worker_threads(world) // max(1, world)) if a.C == 1 else 0
+    # -C 1 under torchrun: a CPU worker thread per rank (ref NB_THREADS_GPU - 1 threads).
+    # The host's cores are shared by the ranks of THIS node (LOCAL_WORLD_SIZE), not by
+    # the whole job: on several nodes the global WORLD_SIZE would under-provision them.
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    cpu = max(1, _cpu_worker_threads(local) // max(1, local)) if a.C == 1 else 0
     return {"problem": "pfsp", "inst": a.inst, "lb": a.lb, "ub": a.ub, "backend": "gpu",
             "engine": {"max_parents": a.max_parents, "ring_bytes": int(a.ring_gb * (1 << 30)),
                        "streams": max(1, a.streams)},
@@ -214,11 +217,13 @@ def pfsp_main(argv: list[str]) -> int:
     print("\nExploration terminated.")
     print(report.pfsp_results(res["best"], res["tree"], res["sol"], res["elapsed"]))
     workers = [report.WorkerStats(**w) for w in res["workers"]]
+    # C column: 1 when every rank ran a CPU worker next to its GPU (hybrid rank engine)
+    C = 1 if spec["dist"]["cpu_workers"] > 0 else 0
     if not a.no_csv:
-        report.write_multi_gpu_csv(os.path.join(a.csv_dir, "multigpu.csv"), a.inst, a.lb, D, 0, a.ws, res["best"],
+        report.write_multi_gpu_csv(os.path.join(a.csv_dir, "multigpu.csv"), a.inst, a.lb, D, C, a.ws, res["best"],
                                    a.m, a.M, a.T, res["elapsed"], res["tree"], res["sol"], workers)
         # one process per GPU = the reference's distributed driver layout (one GPU per rank)
-        report.write_dist_multi_gpu_csv(os.path.join(a.csv_dir, "dist_multigpu.csv"), a.inst, a.lb, 1, 0, a.L, D,
+        report.write_dist_multi_gpu_csv(os.path.join(a.csv_dir, "dist_multigpu.csv"), a.inst, a.lb, 1, C, a.L, D,
                                         res["best"], a.m, a.M, a.T, res["elapsed"], res["tree"], res["sol"], workers,
                                         [w.dist_load_bal for w in workers], [w.t_load_bal for w in workers])
     if a.json:

@@ -231,6 +231,7 @@ class MultiEngine final : public IEngine {
       end_.store(false);
       running_.store(static_cast<int>(e_.size()));
       caller_stop_ = false;
+      slice_stop_below_ = stop_below;
       {
         std::lock_guard<std::mutex> lk(mu_);
         slice_left_ = left;
@@ -239,7 +240,17 @@ class MultiEngine final : public IEngine {
         ++slice_id_;
         cv_.notify_all();
       }
-      launches += run_sub(0, left);
+      try {
+        launches += run_sub(0, left);
+      } catch (...) {
+        // end the slice for the worker threads and let them drain before unwinding:
+        // the caller must not touch the sub-engines while they still run
+        e_[0]->set_progress_hook(nullptr);
+        end_.store(true, std::memory_order_release);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return pending_ == 0; });
+        throw;
+      }
       {
         std::unique_lock<std::mutex> lk(mu_);
         done_cv_.wait(lk, [&] { return pending_ == 0; });
@@ -264,10 +275,12 @@ class MultiEngine final : public IEngine {
       while (b < cur && !best_.compare_exchange_weak(cur, b, std::memory_order_acq_rel)) {
       }
       if (cur < b) b = cur;
-      if (i == 0 && hook_) {
+      if ((i == 0 && hook_) || slice_stop_below_ > 1) {
         size_t tot = 0;
         for (auto& s : sizes_) tot += s.load(std::memory_order_relaxed);
-        if (hook_(tot, b)) {
+        // the caller's stop_below holds inside a slice too (summed live pool sizes)
+        if (slice_stop_below_ > 1 && tot < slice_stop_below_) end_.store(true, std::memory_order_release);
+        if (i == 0 && hook_ && hook_(tot, b)) {
           caller_stop_ = true;
           end_.store(true, std::memory_order_release);
         }
@@ -420,6 +433,7 @@ class MultiEngine final : public IEngine {
   bool quit_ = false;
   unsigned long long slice_id_ = 0;
   double slice_left_ = 0;
+  std::atomic<size_t> slice_stop_below_{0};  // run()'s stop_below, applied inside a slice
   int pending_ = 0;
   std::vector<std::exception_ptr> errors_;
   void* buf_ = nullptr;

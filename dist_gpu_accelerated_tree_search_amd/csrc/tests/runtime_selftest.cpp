@@ -5,7 +5,10 @@
 //     watchdog thread, fault injection)
 //   * multithreaded CpuEngine batches
 // Build: g++ -O1 -g -fsanitize=thread (or address,undefined) ... ; exit code 0 = pass.
+#include <chrono>
 #include <cstdio>
+#include <stdexcept>
+#include <thread>
 #include <memory>
 #include <vector>
 
@@ -128,6 +131,55 @@ int main() {
     while (me.size() > 0) me.run(-1, 0.001, 1);
     const EngineStats s2 = me.stats();
     CHECK(s2.tree == seq_ub.tree && s2.sol == seq_ub.sol);
+  }
+  {  // sub-engine 0 throws inside a slice: run() rethrows only after the worker threads
+     // have left their slices (no sub-engine still running when the caller unwinds)
+    struct Throwing final : IEngine {
+      IEngine* inner;
+      std::atomic<int> calls{0};
+      explicit Throwing(IEngine* e) : inner(e) {}
+      size_t node_bytes() const override { return inner->node_bytes(); }
+      void push_host(const void* n, size_t k) override { inner->push_host(n, k); }
+      size_t pop_host(void* o, size_t k) override { return inner->pop_host(o, k); }
+      size_t export_device(void* d, size_t k) override { return inner->export_device(d, k); }
+      void import_device(const void* s, size_t k) override { inner->import_device(s, k); }
+      size_t size() override { return inner->size(); }
+      long run(long a, double b, size_t c) override {
+        if (++calls >= 12) throw std::runtime_error("injected sub-engine failure");
+        return inner->run(std::min<long>(a < 0 ? 4 : a, 4), b, c);
+      }
+      void begin(const void* n, size_t k, int b) override { inner->begin(n, k, b); }
+      EngineStats solve_from(const void* n, size_t k, int b) override { return inner->solve_from(n, k, b); }
+      size_t warm_split(int r, int w, size_t win, int p) override { return inner->warm_split(r, w, win, p); }
+      void set_split(int r, int w, size_t mp) override { inner->set_split(r, w, mp); }
+      bool split_pending() override { return inner->split_pending(); }
+      void set_progress_hook(ProgressHook h) override { inner->set_progress_hook(std::move(h)); }
+      void set_best(int b) override { inner->set_best(b); }
+      int best() override { return inner->best(); }
+      void reset_counters() override { inner->reset_counters(); }
+      EngineStats stats() override { return inner->stats(); }
+      void synchronize() override {}
+      uintptr_t stream() const override { return 0; }
+      int device() const override { return -1; }
+    };
+    CpuEngine<PfspFrontProblem<5>> a(PfspFrontProblem<5>(in, 0), 16, 1), b(PfspFrontProblem<5>(in, 0), 16, 1);
+    Throwing ta(&a);
+    MultiConfig mc3;
+    mc3.needy_below = 8;
+    mc3.donor_min = 32;
+    MultiEngine me({&ta, &b}, nullptr, mc3);
+    const auto root = PfspFrontProblem<5>(in, 0).root();
+    bool threw = false;
+    try {
+      (void)me.solve_from(&root, 1, seq.best);
+    } catch (const std::runtime_error&) {
+      threw = true;
+    }
+    CHECK(threw);
+    const size_t s1 = b.size();  // the worker has left its slice: its pool no longer changes
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    CHECK(b.size() == s1);
+    std::printf("multi with a throwing sub-engine: rethrown %d, worker pool stable at %zu\n", threw ? 1 : 0, s1);
   }
   std::printf(failures ? "SELFTEST FAILED\n" : "SELFTEST OK\n");
   return failures ? 1 : 0;

@@ -79,4 +79,4 @@ class QueensModel:
         return ops.require_gpu(device).queens_labels(self.N, self.G, np.ascontiguousarray(nodes, np.uint8), device)
 
     def describe(self) -> dict:
-        return {"problem": "nqueens", "N": self.N, "G": self.G}
+        return {"problem": "nqueens", "N": self.N, "G": self.G, "layout": "bitmask"}

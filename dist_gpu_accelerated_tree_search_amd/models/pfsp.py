@@ -189,5 +189,7 @@ class PfspModel:
                              np.ascontiguousarray(nodes, dtype=np.uint8), int(best), device)
 
     def describe(self) -> dict:
+        # the node layout is part of the identity: a 20-job front node (<= 10 machines) and a
+        # 20-job permutation node are both 32 B, so node_bytes alone cannot tell them apart
         return {"problem": "pfsp", "inst": self.inst_id, "jobs": self.jobs, "machines": self.machines, "lb": self.lb,
-                "best_known": self.best_known}
+                "best_known": self.best_known, "layout": "front" if self.front_layout else "perm"}
