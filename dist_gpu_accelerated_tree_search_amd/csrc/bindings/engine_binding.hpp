@@ -310,7 +310,34 @@ struct PyDistSession {
 // dist_rounds(engine, shm_address | allgather_fn, rank, world, options, transfer_fn,
 //             round_hook, rounds0, timeout_s) -> dict (core/dist_rounds.hpp)
 // DistSession(engine, model, ...).solve(best) -> one native cooperative solve (core/dist_session.hpp)
-inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory) {
+// A native transport object (HIP module: RcclTransport) in place of a Python
+// transfer callable: returns an empty TransferFn when `obj` is not one.
+using NativeTransfer = std::function<TransferFn(py::object obj, IEngine* e)>;
+
+inline TransferFn resolve_transfer(const NativeTransfer& native, py::object obj, IEngine* e) {
+  if (native) {
+    TransferFn f = native(obj, e);
+    if (f) return f;
+  }
+  return transfer_from(obj);
+}
+
+inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory, NativeTransfer native = {}) {
+  m.def(
+      "p2p_calls",
+      [](py::list plan, int rank) {
+        Plan pl;
+        for (auto t : plan) {
+          auto x = t.cast<py::tuple>();
+          pl.push_back({x[0].cast<int>(), x[1].cast<int>(), x[2].cast<size_t>()});
+        }
+        py::list out;
+        for (const auto& c : p2p_calls(pl, rank))
+          out.append(py::make_tuple(c.send ? "send" : "recv", c.peer, c.offset, c.count));
+        return out;
+      },
+      py::arg("plan"), py::arg("rank"),
+      "This rank's grouped point-to-point calls for a transfer plan (csrc/core/dist_rounds.hpp p2p_calls).");
   m.def(
       "plan_transfers",
       [](std::vector<int64_t> sizes, size_t needy_below, size_t donor_min, size_t cap, int local_world, bool intra,
@@ -324,11 +351,11 @@ inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory) {
       py::arg("intra") = true, py::arg("inter") = true);
   m.def(
       "dist_rounds",
-      [](IEngine& e, uintptr_t shm_address, py::object allgather_fn, int rank, int world, py::dict o,
+      [native](IEngine& e, uintptr_t shm_address, py::object allgather_fn, int rank, int world, py::dict o,
          py::object transfer_fn, py::object round_hook, unsigned long long rounds0, double timeout_s) {
         const DistOptions opt = dist_options_from(o);
         auto ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s);
-        const TransferFn xfer = transfer_from(transfer_fn);
+        const TransferFn xfer = resolve_transfer(native, transfer_fn, &e);
         const RoundHook hook = hook_from(round_hook);
         DistOutcome out;
         {
@@ -342,7 +369,7 @@ inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory) {
       py::arg("timeout_s") = 1800.0,
       "Native lock-step rounds of a multi-rank solve until every pool is empty (or max_rounds).");
   py::class_<PyDistSession>(m, "DistSession", py::module_local())
-      .def(py::init([warmup_factory](py::object engine, py::object model, uintptr_t shm_address, py::object allgather_fn,
+      .def(py::init([warmup_factory, native](py::object engine, py::object model, uintptr_t shm_address, py::object allgather_fn,
                                      int rank, int world, py::dict o, py::object transfer_fn, py::object round_hook,
                                      size_t warm_target, size_t split_min, double timeout_s, bool split) {
              auto s = std::make_unique<PyDistSession>();
@@ -352,7 +379,7 @@ inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory) {
              s->ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s);
              s->opt = dist_options_from(o);
              s->warm = warmup_factory(model);
-             s->xfer = transfer_from(transfer_fn);
+             s->xfer = resolve_transfer(native, transfer_fn, s->e);
              s->hook = hook_from(round_hook);
              s->warm_target = warm_target;
              s->split_min = split_min;

@@ -230,6 +230,25 @@ PYBIND11_MODULE(_tts_cpu, m) {
       },
       py::arg("inst"), py::arg("lb"), py::arg("best"), py::arg("target"));
   m.def(
+      "pfsp_bfs_level",
+      [](const PfspInstance& in, int lb, int best, int depth) {
+        // every node of tree level `depth` (engine layout), level by level from the root
+        // with a fixed incumbent (analysis and kernel timing windows)
+        return with_pfsp_problem(in, lb, [&](auto prob) {
+          using Node = typename decltype(prob)::Node;
+          std::vector<Node> cur{prob.root()}, nxt;
+          u64 tree = 0, sol = 0;
+          int b = best;
+          for (int d = 0; d < depth && !cur.empty(); ++d) {
+            nxt.clear();
+            for (const Node& x : cur) prob.decompose(x, b, tree, sol, [&](const Node& c) { nxt.push_back(c); });
+            std::swap(cur, nxt);
+          }
+          return nodes_to_array(cur.data(), cur.size());
+        });
+      },
+      py::arg("inst"), py::arg("lb"), py::arg("best"), py::arg("depth"));
+  m.def(
       "lb2_child_profile",
       [](const PfspInstance& in, U8 nodes, int best) {
         // analysis helper: for every child of every node (LB2 work model of the expand

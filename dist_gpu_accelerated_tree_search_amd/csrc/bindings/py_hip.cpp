@@ -14,6 +14,7 @@
 #include "../hip/host_support.hpp"
 #include "../hip/pfsp_engine.hpp"
 #include "../hip/queens_engine.hpp"
+#include "../hip/rccl_transport.hpp"
 #include "engine_binding.hpp"
 
 namespace py = pybind11;
@@ -43,6 +44,69 @@ PYBIND11_MODULE(_tts_hip, m) {
   m.doc() = "gfx950 (MI355X) device engines: device-resident pools, fused bound/prune/compact kernels, hipGraphs.";
   bind_engine(m);
   bind_shm_control(m);
+  py::class_<RcclTransport>(m, "RcclTransport")
+      .def(py::init([](py::bytes id, int rank, int world, int device) {
+             const std::string s = id;
+             const std::vector<uint8_t> v(s.begin(), s.end());
+             py::gil_scoped_release nogil;  // ncclCommInitRank waits for every rank
+             return std::make_unique<RcclTransport>(v, rank, world, device);
+           }),
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
+      .def_static("new_id", []() {
+        const std::vector<uint8_t> v = RcclTransport::new_id();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def(
+          "execute",
+          [](RcclTransport& t, py::list plan, IEngine& e) {
+            Plan pl;
+            for (auto x : plan) {
+              auto tt = x.cast<py::tuple>();
+              pl.push_back({tt[0].cast<int>(), tt[1].cast<int>(), tt[2].cast<size_t>()});
+            }
+            py::gil_scoped_release nogil;
+            return t.execute(pl, e);
+          },
+          py::arg("plan"), py::arg("engine"),
+          "This rank's part of a transfer plan: export -> grouped ncclSend/ncclRecv on the engine's transfer "
+          "stream -> import; (sent, received).")
+      .def(
+          "self_loop",
+          [](RcclTransport& t, IEngine& e, size_t n) {
+            py::gil_scoped_release nogil;
+            return t.self_loop(e, n);
+          },
+          py::arg("engine"), py::arg("n"))
+      .def(
+          "preflight",
+          [](RcclTransport& t, size_t nbytes, bool corrupt) {
+            std::pair<int, double> r;
+            {
+              py::gil_scoped_release nogil;
+              r = t.preflight(nbytes, corrupt);
+            }
+            py::dict d;
+            d["ok"] = true;
+            d["peers"] = r.first;
+            d["bytes_per_peer"] = nbytes / 4 * 4;
+            d["seconds"] = r.second;
+            d["GBps"] = r.second > 0 ? r.first * static_cast<double>(nbytes) / r.second / 1e9 : 0.0;
+            d["native"] = true;
+            return d;
+          },
+          py::arg("nbytes") = size_t(4) << 20, py::arg("corrupt") = false)
+      .def_property_readonly("rank", &RcclTransport::rank)
+      .def_property_readonly("world", &RcclTransport::world)
+      .def_property_readonly("device", &RcclTransport::device)
+      .def_property_readonly("transfers", &RcclTransport::transfers)
+      .def_property_readonly("bytes_sent", &RcclTransport::bytes_sent)
+      .def_property_readonly("bytes_recv", &RcclTransport::bytes_recv);
+  const NativeTransfer native_rccl = [](py::object obj, IEngine* e) -> TransferFn {
+    if (!py::isinstance<RcclTransport>(obj)) return {};
+    RcclTransport* t = obj.cast<RcclTransport*>();
+    // the Python object stays referenced by the caller (DistSolver / dist_rounds call)
+    return [t, e](const Plan& p) { return t->execute(p, *e); };
+  };
   bind_dist_rounds(m, [](py::object model) -> WarmupFn {
     if (py::hasattr(model, "native")) {
       auto inst = std::make_shared<PfspInstance>(make_instance(model.attr("jobs").cast<int>(),
@@ -52,7 +116,7 @@ PYBIND11_MODULE(_tts_hip, m) {
       return with_pfsp_problem(*inst, lb, [&](auto prob) -> WarmupFn { return make_warmup(inst, prob); });
     }
     return make_warmup(nullptr, QueensProblem(model.attr("N").cast<int>(), model.attr("G").cast<int>()));
-  });
+  }, native_rccl);
   bind_runner(
       m, []() -> std::unique_ptr<DeviceStaging> { return std::make_unique<HipStaging>(); }, &device_cpus);
   if (!std::getenv("TTS_NO_ROCTX")) install_roctx_hooks();
@@ -199,6 +263,82 @@ PYBIND11_MODULE(_tts_hip, m) {
       "Time one expand iteration over this window (LB2): min/median ms over reps launches on the engine's grid, "
       "and per-chunk shader clocks of phases A, B1, B2, B3+C from one instrumented launch.");
 
+  m.def(
+      "pfsp_front_probe",
+      [](int jobs, int machines, std::vector<int> p, int lb, U8 nodes, int best, int device, size_t max_parents,
+         int fuse_max, int deep_levels, int deep_per3, int deep_per4, int local_steps, unsigned cap, int split_rank,
+         int split_world, size_t split_min) {
+        const PfspInstance in = make_instance(jobs, machines, std::move(p));
+        EngineConfig c;
+        c.device = device;
+        c.max_parents = max_parents;
+        c.ring_bytes = size_t(1) << 30;
+        c.fuse_max = fuse_max;
+        c.deep_levels = deep_levels;
+        c.deep_per3 = deep_per3;
+        c.deep_per4 = deep_per4;
+        c.local_steps = local_steps;
+        FrontProbeResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = pfsp_front_probe(in, lb, nodes.data(), static_cast<size_t>(nodes.shape(0)), best, c, cap, split_rank,
+                               split_world, split_min);
+        }
+        py::dict d;
+        d["records"] = r.records;
+        d["checked"] = r.checked;
+        py::dict k;
+        const char* names[5] = {"one_level", "child_parallel", "thread_per_node", "local_dfs", "split"};
+        for (int i = 0; i < 5; ++i) k[names[i]] = r.by_kind[i];
+        d["by_kind"] = k;
+        d["bad_lb"] = r.bad_lb;
+        d["bad_remain"] = r.bad_remain;
+        d["bad_job"] = r.bad_job;
+        d["first_bad"] = r.first_bad;
+        d["tree"] = r.st.tree;
+        d["sol"] = r.st.sol;
+        d["best"] = r.st.best;
+        d["iters"] = r.st.iters;
+        return d;
+      },
+      py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("nodes"), py::arg("best"),
+      py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 16, py::arg("fuse_max") = 1 << 30,
+      py::arg("deep_levels") = 4, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("local_steps") = 4,
+      py::arg("cap") = 1u << 22, py::arg("split_rank") = 0, py::arg("split_world") = 1, py::arg("split_min") = 0,
+      "A complete front-kernel engine solve from these (front-layout) nodes with probe records on: every child "
+      "bound of every iteration shape checked against the host oracle (counts of records and mismatches).");
+  m.def(
+      "pfsp_front_time",
+      [](int jobs, int machines, std::vector<int> p, int lb, U8 nodes, int best, int device, size_t max_parents,
+         int fuse_max, int deep_levels, int deep_per3, int deep_per4, int reps) {
+        const PfspInstance in = make_instance(jobs, machines, std::move(p));
+        EngineConfig c;
+        c.device = device;
+        c.max_parents = max_parents;
+        c.fuse_max = fuse_max;
+        c.deep_levels = deep_levels;
+        c.deep_per3 = deep_per3;
+        c.deep_per4 = deep_per4;
+        std::vector<double> t;
+        {
+          py::gil_scoped_release nogil;
+          t = pfsp_front_time(in, lb, nodes.data(), static_cast<size_t>(nodes.shape(0)), best, c, reps);
+        }
+        py::dict d;
+        d["ms_min"] = t[0];
+        d["ms_median"] = t[1];
+        d["grid"] = static_cast<int>(t[2]);
+        d["nch_out"] = static_cast<int>(t[3]);
+        const size_t nblk = (t.size() - 4) / 16;
+        py::array_t<double> tl({static_cast<py::ssize_t>(nblk), static_cast<py::ssize_t>(16)});
+        std::memcpy(tl.mutable_data(), t.data() + 4, nblk * 16 * sizeof(double));
+        d["stamps_us"] = tl;
+        return d;
+      },
+      py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("nodes"), py::arg("best"),
+      py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 19, py::arg("fuse_max") = 1 << 30,
+      py::arg("deep_levels") = 4, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("reps") = 20,
+      "Time one front-kernel iteration over this window: min / median ms, and the per-workgroup phase stamps.");
   m.def(
       "queens_labels",
       [](int N, int G, U8 parents, int device) {

@@ -150,6 +150,39 @@ inline Plan plan_transfers(const std::vector<int64_t>& sizes, size_t needy_below
                         std::vector<size_t>(n, cap), local_world, intra, inter);
 }
 
+// One rank's part of a transfer plan as grouped point-to-point calls, in plan order:
+// as a donor it sends consecutive slices of its exported block (one export of all its
+// outgoing nodes), as a receiver it receives consecutive slices of its staging block.
+// Every rank derives its calls from the same plan, so each send has its matching
+// receive on the peer inside the same group (RCCL ncclGroupStart / ncclSend /
+// ncclRecv / ncclGroupEnd, csrc/hip/rccl_transport.hpp; the reference's Allgatherv of
+// every donor's nodes to every rank, pfsp_dist_multigpu_cuda.c:122-137, becomes
+// targeted pairs only).
+struct P2PCall {
+  bool send;
+  int peer;
+  size_t offset, count;  // in nodes, within this rank's out (send) or in (recv) block
+};
+inline std::vector<P2PCall> p2p_calls(const Plan& plan, int rank, size_t* total_out = nullptr,
+                                      size_t* total_in = nullptr) {
+  std::vector<P2PCall> calls;
+  size_t out = 0, in = 0;
+  for (const auto& t : plan) {
+    if (t.n == 0 || t.donor == t.receiver) continue;
+    if (t.donor == rank) {
+      calls.push_back({true, t.receiver, out, t.n});
+      out += t.n;
+    }
+    if (t.receiver == rank) {
+      calls.push_back({false, t.donor, in, t.n});
+      in += t.n;
+    }
+  }
+  if (total_out) *total_out = out;
+  if (total_in) *total_in = in;
+  return calls;
+}
+
 struct DistOptions {
   size_t needy_below = 25;   // a rank below this many nodes asks for work
   size_t donor_min = 50;     // a donor holds at least this many

@@ -28,6 +28,9 @@ struct EngineConfig {
   int iters_first = 18;                  // first replay after begin(): covers a 20-job tree in one graph
   int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
   int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
+  int deep_levels = 4;                   // fused iterations: at most this many tree levels (kernels that have them)
+  int deep_per3 = 8;                     // ... 3 levels when a workgroup takes at most this many parents
+  int deep_per4 = 2;                     // ... 4 levels when a workgroup takes at most this many parents
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };

@@ -123,6 +123,14 @@ class DeviceEngine final : public IEngine {
     if (const char* f = std::getenv("TTS_LOCAL_STEPS")) pa.local_steps = std::min(std::max(0, std::atoi(f)), Traits::kLocalSteps);
     pa.local_min = 0;
     if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
+    // multi-level fused iterations (kernels with LMAX > 2): 3 levels up to deep_per[0]
+    // parents per workgroup, 4 up to deep_per[1]; TTS_DEEP_LEVELS / _P3 / _P4 for A/B runs
+    pa.deep_levels = cfg_.deep_levels;
+    pa.deep_per[0] = cfg_.deep_per3;
+    pa.deep_per[1] = cfg_.deep_per4;
+    if (const char* f = std::getenv("TTS_DEEP_LEVELS")) pa.deep_levels = std::max(2, std::atoi(f));
+    if (const char* f = std::getenv("TTS_DEEP_P3")) pa.deep_per[0] = std::max(0, std::atoi(f));
+    if (const char* f = std::getenv("TTS_DEEP_P4")) pa.deep_per[1] = std::max(0, std::atoi(f));
     grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, resident)));
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known

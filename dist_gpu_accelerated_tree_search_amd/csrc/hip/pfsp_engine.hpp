@@ -78,7 +78,7 @@ struct PfspFrontTraits {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_front_kernel<M>, dev::kBlock, 0) != hipSuccess)
       return 1;
-    return n;
+    return std::min(n, G::WAVES);  // FrontGeom::WAVES: the API over-reports by one
   }
 };
 
@@ -95,6 +95,8 @@ inline std::vector<uint16_t> pfsp_front_fill_args(const PfspInstance& in, dev::P
   a.jobs = in.jobs;
   for (int m = 0; m < M; ++m) a.min_tails[m] = t.tails[m];
   a.bpf = dev::FrontGeom<M>::BPF;
+  a.cp_max = dev::FrontGeom<M>::CPMAX;
+  if (const char* f = std::getenv("TTS_CP_MAX")) a.cp_max = std::max(0, std::atoi(f));  // A/B runs
   if (const char* f = std::getenv("TTS_FUSED_BPF"))  // A/B runs
     a.bpf = std::min(std::max(1, std::atoi(f)), dev::FrontGeom<M>::BPF_CP);
   return ptab;
@@ -461,6 +463,184 @@ std::unique_ptr<IEngine> make_pfsp_front_engine_t(const PfspInstance& in, const 
   return eng;
 }
 
+// Element-wise probe of the production LB1 / LB1_d front kernel (tests):
+// a complete engine solve from `nodes` (front layout) with the kernel's probe records
+// on, so every iteration shape the solve takes — one level per kernel, the split
+// iteration, multi-level chunks (child-parallel and thread-per-node levels with carried
+// remains), local DFS — records each child it bounds: the parent's words, the parent's
+// remain as the kernel holds it, the job and the bound. Every record is checked here
+// against the host oracle (PfspFrontProblem: ref add_front_and_bound,
+// c_bound_simple.c:219-244). At most `cap` records are kept and checked; the count of
+// all records is returned too.
+struct FrontProbeResult {
+  unsigned long long records = 0, checked = 0;
+  unsigned long long by_kind[5] = {};
+  unsigned long long bad_lb = 0, bad_remain = 0, bad_job = 0;
+  EngineStats st;
+  std::vector<uint32_t> first_bad;
+};
+template <int M>
+FrontProbeResult pfsp_front_probe_t(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
+                                    const EngineConfig& cfg, unsigned cap, int split_rank, int split_world,
+                                    size_t split_min) {
+  using G = dev::FrontGeom<M>;
+  using Node = PfspFrontNode<M>;
+  TTS_HIP_CHECK(hipSetDevice(cfg.device));
+  const PfspFrontProblem<M> prob(in, lb);
+  dev::PfspFrontArgs<M> a{};
+  const std::vector<uint16_t> ptab = pfsp_front_fill_args(in, a);
+  a.ptab = upload_vec(ptab);
+  uint32_t* drec = nullptr;
+  unsigned* dn = nullptr;
+  TTS_HIP_CHECK(hipMalloc(&drec, std::max<size_t>(1, cap) * G::DBGW * sizeof(uint32_t)));
+  TTS_HIP_CHECK(hipMalloc(&dn, sizeof(unsigned)));
+  TTS_HIP_CHECK(hipMemset(dn, 0, sizeof(unsigned)));
+  a.dbg_rec = drec;
+  a.dbg_n = dn;
+  a.dbg_cap = cap;
+  FrontProbeResult res;
+  {
+    DeviceEngine<PfspFrontTraits<M>> eng(cfg, a);
+    if (split_world > 1) eng.set_split(split_rank, split_world, split_min);
+    res.st = eng.solve_from(nodes, n, best);
+  }
+  unsigned total = 0;
+  TTS_HIP_CHECK(hipMemcpy(&total, dn, sizeof(unsigned), hipMemcpyDeviceToHost));
+  res.records = total;
+  const size_t keep = std::min<size_t>(total, cap);
+  std::vector<uint32_t> rec(keep * G::DBGW);
+  if (keep) TTS_HIP_CHECK(hipMemcpy(rec.data(), drec, rec.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  (void)hipFree(drec);
+  (void)hipFree(dn);
+  (void)hipFree(const_cast<uint16_t*>(a.ptab));
+  res.checked = keep;
+  for (size_t i = 0; i < keep; ++i) {
+    const uint32_t* r = &rec[i * G::DBGW];
+    const int j = static_cast<int>(r[0] & 0xffu), kind = static_cast<int>((r[0] >> 8) & 0xffu);
+    if (kind < 5) ++res.by_kind[kind];
+    Node parent;
+    std::memcpy(&parent, r + 2, sizeof(Node));
+    bool bad = false;
+    if (j >= 32 || !((parent.rest >> j) & 1u)) {
+      ++res.bad_job;
+      bad = true;
+    } else {
+      int rt[M];
+      prob.remain_tail(parent, rt);
+      for (int m = 0; m < M; ++m) {
+        const int got = static_cast<int>((r[2 + G::NW + (m >> 1)] >> ((m & 1) * 16)) & 0xffffu);
+        if (got != rt[m] - prob.tab.tails[m]) {
+          ++res.bad_remain;
+          bad = true;
+          break;
+        }
+      }
+      if (prob.child(parent, rt, j, nullptr) != static_cast<int>(r[1])) {
+        ++res.bad_lb;
+        bad = true;
+      }
+    }
+    if (bad && res.first_bad.empty()) res.first_bad.assign(r, r + G::DBGW);
+  }
+  return res;
+}
+
+// Timing probe of ONE front-kernel iteration over a given window (the nodes loaded as
+// the pool), on the engine's grid: `reps` launches from the same state (min / median
+// ms), then one launch with the per-workgroup phase stamps (front_stamp). Returns
+// {ms_min, ms_median, grid, iteration levels, then grid x 16 stamps in us from the first
+// workgroup entry (0 where a stamp was not reached)}.
+template <int M>
+std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
+                                      const EngineConfig& cfg, int reps) {
+  using G = dev::FrontGeom<M>;
+  using Node = PfspFrontNode<M>;
+  TTS_HIP_CHECK(hipSetDevice(cfg.device));
+  (void)lb;
+  dev::PfspFrontArgs<M> a{};
+  const std::vector<uint16_t> ptab = pfsp_front_fill_args(in, a);
+  std::vector<void*> owned;
+  auto dalloc = [&](size_t bytes) {
+    void* d = nullptr;
+    TTS_HIP_CHECK(hipMalloc(&d, std::max<size_t>(bytes, 16)));
+    TTS_HIP_CHECK(hipMemset(d, 0, std::max<size_t>(bytes, 16)));
+    owned.push_back(d);
+    return d;
+  };
+  a.ptab = upload_vec(ptab);
+  owned.push_back(const_cast<uint16_t*>(a.ptab));
+  const size_t max_chunks = std::min<size_t>((cfg.max_parents + G::BP - 1) / G::BP, G::MAXCHUNKS);
+  size_t cap = 1;
+  while (cap < n) cap *= 2;
+  auto& pa = a.pool;
+  pa.ring = static_cast<Node*>(dalloc(cap * sizeof(Node)));
+  for (int b = 0; b < 2; ++b) {
+    pa.buf[b] = static_cast<Node*>(dalloc(max_chunks * G::SLOT * sizeof(Node)));
+    pa.cnt[b] = static_cast<int*>(dalloc(max_chunks * sizeof(int)));
+    pa.lcnt[b] = static_cast<int*>(dalloc(max_chunks * sizeof(int)));
+  }
+  dev::PoolCtl h{};
+  h.slot[0].stack = n;
+  h.best.v = best;
+  pa.ctl = static_cast<dev::PoolCtl*>(dalloc(sizeof(dev::PoolCtl)));
+  pa.mirror = nullptr;
+  pa.cap_mask = cap - 1;
+  pa.max_parents = static_cast<int>(max_chunks * G::BP);
+  pa.max_chunks = static_cast<int>(max_chunks);
+  pa.fuse_max = cfg.fuse_max;
+  pa.local_steps = std::min(cfg.local_steps, G::LT);
+  pa.deep_levels = cfg.deep_levels;
+  pa.deep_per[0] = cfg.deep_per3;
+  pa.deep_per[1] = cfg.deep_per4;
+  int bpc = 0, cus = 0;
+  bpc = PfspFrontTraits<M>::blocks_per_cu();
+  if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(g));  // as DeviceEngine
+  TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device));
+  const int grid = static_cast<int>(std::min<size_t>(max_chunks, static_cast<size_t>(std::max(1, bpc)) * cus));
+  auto restore = [&] {
+    TTS_HIP_CHECK(hipMemcpy(pa.ring, nodes, n * sizeof(Node), hipMemcpyHostToDevice));
+    TTS_HIP_CHECK(hipMemcpy(pa.ctl, &h, sizeof(h), hipMemcpyHostToDevice));
+  };
+  hipEvent_t e0, e1;
+  TTS_HIP_CHECK(hipEventCreate(&e0));
+  TTS_HIP_CHECK(hipEventCreate(&e1));
+  std::vector<double> ms;
+  for (int r = 0; r < std::max(1, reps); ++r) {
+    restore();
+    TTS_HIP_CHECK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, 0, a, 0);
+    TTS_HIP_CHECK(hipGetLastError());
+    TTS_HIP_CHECK(hipEventRecord(e1, 0));
+    TTS_HIP_CHECK(hipEventSynchronize(e1));
+    float t = 0;
+    TTS_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+    ms.push_back(t);
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  std::sort(ms.begin(), ms.end());
+  restore();
+  a.dbg_blk = static_cast<unsigned long long*>(dalloc(static_cast<size_t>(grid) * 16 * sizeof(unsigned long long)));
+  hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, 0, a, 0);
+  TTS_HIP_CHECK(hipGetLastError());
+  TTS_HIP_CHECK(hipDeviceSynchronize());
+  std::vector<unsigned long long> blk(static_cast<size_t>(grid) * 16);
+  TTS_HIP_CHECK(hipMemcpy(blk.data(), a.dbg_blk, blk.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  dev::PoolCtl after{};
+  TTS_HIP_CHECK(hipMemcpy(&after, pa.ctl, sizeof(after), hipMemcpyDeviceToHost));
+  for (void* d : owned) (void)hipFree(d);
+  int rate_khz = 0;
+  TTS_HIP_CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, cfg.device));
+  unsigned long long t0 = ~0ull;
+  for (int i = 0; i < grid; ++i)
+    if (blk[16 * i]) t0 = std::min(t0, blk[16 * i]);
+  const double us = 1e3 / std::max(1, rate_khz);
+  std::vector<double> out = {ms.front(), ms[ms.size() / 2], static_cast<double>(grid),
+                             static_cast<double>(after.slot[1].nch)};
+  for (unsigned long long x : blk) out.push_back(x ? static_cast<double>(x - t0) * us : 0.0);
+  return out;
+}
+
 // Bounds of permutation-layout parents through the front kernel (tests): parents are
 // converted on the host, bounds come back in the permutation's child order k = depth..N-1.
 template <int M>
@@ -520,6 +700,12 @@ std::unique_ptr<IEngine> make_pfsp_engine(const PfspInstance& in, int lb, const 
 std::vector<int> pfsp_gpu_bounds(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device);
 std::vector<int> pfsp_expand_probe(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device,
                                    int variant, int reps = 0, std::vector<double>* timing = nullptr);
+std::vector<double> pfsp_front_time(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
+                                    const EngineConfig& cfg, int reps);
+// front-layout instances only (pfsp_front_ok), defined with the 20-job bucket
+FrontProbeResult pfsp_front_probe(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
+                                  const EngineConfig& cfg, unsigned cap, int split_rank = 0, int split_world = 1,
+                                  size_t split_min = 0);
 
 #define TTS_PFSP_DECLARE_BUCKET(NJ)                                                                   \
   std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg); \

@@ -40,12 +40,27 @@ struct FrontGeom {
   static constexpr int LT = 8;                          // local DFS steps per chunk at most
   static constexpr int SLOT = 2 * MAXCH;                // chunk slot region = its private stack
   static constexpr int MAXCHUNKS = 2048;
-  // two-level chunks (front_two_level_cp): up to BPF_CP parents, spread over the grid
-  // (pool_begin); level-1 survivors past kBlock go out unexpanded, so the chunk's output
-  // stays within SLOT
+  // multi-level chunks (front_multi_level): up to BPF_CP parents, spread over the grid
+  // (pool_begin), expanded LMAX levels deep at most; a level's survivors past CAP go out
+  // unexpanded, so the chunk's output stays within SLOT
   static constexpr int BPF = 12;     // default cap: two-level windows up to 12 x 2048 parents
   static constexpr int BPF_CP = 32;
-  static constexpr int MID = M > 10 ? 96 : 128;  // level-1 survivors expanded in place (the rest go out)
+  // nodes of one level kept in LDS (the rest go out): sized so that 7 workgroups of the
+  // kernel fit a CU's 160 KB of LDS (the grid is 7 per CU; an 8th-of-LDS overshoot made
+  // one workgroup per CU wait for another to finish)
+  static constexpr int CAP = 96;
+  static constexpr int LMAX = 4;
+  // a level of at most CPMAX children is expanded child-parallel (one thread per child),
+  // a wider one one thread per node (each runs its children in turn)
+  static constexpr int CPMAX = 3 * 256;
+  // resident workgroups (= waves per SIMD) the kernel is compiled for; the occupancy API
+  // reports one more than fit at its SGPR count (the SGPR file, 800 per SIMD, holds
+  // 800 / (ceil(sgpr / 16) * 16 + 16) waves), so the engine's grid uses this instead
+  // (measured: a grid of 7 per CU with 6 resident made 256 workgroups start one workgroup
+  // lifetime late, +1.3 us per wide iteration, +4 us per multi-level one)
+  static constexpr int WAVES = M <= 10 ? 6 : 4;
+  // probe records (tests): {job | kind << 8, lb, parent words, parent remain}
+  static constexpr int DBGW = (2 + NW + (M + 1) / 2 + 3) / 4 * 4;
   static constexpr int HW = (M + 1) / 2;  // packed u16 pairs of a p row / a remain
   // u16 row stride of the LDS p table (as PfspConsts::MS): 16 B for M <= 8, else 48 B
   static constexpr int MS = M <= 8 ? 8 : 24;
@@ -65,21 +80,34 @@ struct PfspFrontArgs {
   int* bounds_out;
   int nparents;
   int bpf;  // two-level chunks: at most this many parents (<= FrontGeom::BPF_CP)
+  int cp_max;  // multi-level chunks: child-parallel levels up to this many children
+  // element-wise probe of the search kernel (tests, null in production): every child
+  // bound evaluated by any iteration shape appends a FrontGeom::DBGW-word record
+  uint32_t* dbg_rec;
+  unsigned* dbg_n;
+  unsigned dbg_cap;
+  // per-workgroup phase timeline (timing probe only, null in production): wall clock at
+  // 16 stamps per workgroup (front_stamp)
+  unsigned long long* dbg_blk;
 };
+
+// Timing probe stamp k of this workgroup (thread 0; a.dbg_blk is null in production).
+template <class A>
+__device__ inline void front_stamp(const A& a, int k) {
+  if (a.dbg_blk && threadIdx.x == 0) a.dbg_blk[blockIdx.x * 16 + k] = wall_clock64();
+}
 
 template <int M>
 struct FrontSmem {
   using G = FrontGeom<M>;
   uint16_t ptab[G::NJ][G::MS];
   int scan[kBlock / kWave];
-  // two-level chunks (child-parallel expansion): the chunk's parents and the level-1
-  // survivors expanded in place, each with its remain (unscheduled work per machine,
-  // packed u16 pairs), and the child offsets of the nodes being expanded
-  uint4 par[G::BPF_CP][G::VPN];
-  uint32_t rpar[G::BPF_CP][G::HW];
-  uint4 mid[G::MID][G::VPN];
-  uint32_t rmid[G::MID][G::HW];
-  int coff[G::MID];
+  // multi-level chunks: two levels of nodes (ping-pong), each node with its remain
+  // (unscheduled work per machine, packed u16 pairs), and the child offsets of the
+  // level being expanded
+  uint4 lvl[2][G::CAP][G::VPN];
+  uint32_t rlv[2][G::CAP][G::HW];
+  int coff[G::CAP];
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -120,10 +148,29 @@ __device__ inline void front_store(uint4* dst, const uint32_t (&c)[FrontGeom<M>:
   for (int q = 0; q < FrontGeom<M>::VPN; ++q) dst[q] = make_uint4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
 }
 
+// Probe record of one evaluated child (tests; a.dbg_rec is null in production): the
+// parent's words, its remain (packed u16 pairs, tails excluded), the job, the iteration
+// shape (kind) and the bound. The host recomputes every field (pfsp_front_probe).
+enum FrontDbgKind { kDbgOne = 0, kDbgCp = 1, kDbgTp = 2, kDbgLocal = 3, kDbgSplit = 4 };
+template <int M>
+__device__ inline void front_dbg(const PfspFrontArgs<M>& a, int kind, const uint32_t (&w)[FrontGeom<M>::NW],
+                                 const uint32_t (&rp)[FrontGeom<M>::HW], int j, int lb) {
+  using G = FrontGeom<M>;
+  const unsigned i = atomicAdd(a.dbg_n, 1u);
+  if (i >= a.dbg_cap) return;
+  uint32_t* r = a.dbg_rec + static_cast<size_t>(i) * G::DBGW;
+  r[0] = static_cast<uint32_t>(j) | (static_cast<uint32_t>(kind) << 8);
+  r[1] = static_cast<uint32_t>(lb);
+#pragma unroll
+  for (int k = 0; k < G::NW; ++k) r[2 + k] = w[k];
+#pragma unroll
+  for (int h = 0; h < G::HW; ++h) r[2 + G::NW + h] = rp[h];
+}
+
 // Bounds of every child of the parent held in w: emit(j, lb) for each unscheduled job j.
 template <int M, class Emit>
 __device__ inline void front_parent(const PfspFrontArgs<M>& a, const FrontSmem<M>& sm,
-                                    const uint32_t (&w)[FrontGeom<M>::NW], Emit emit) {
+                                    const uint32_t (&w)[FrontGeom<M>::NW], Emit emit, int kind = kDbgOne) {
   const uint32_t rest = w[1];
   int f[M], r[M];
 #pragma unroll
@@ -148,6 +195,16 @@ __device__ inline void front_parent(const PfspFrontArgs<M>& a, const FrontSmem<M
       const int sv = max(tt, f[m]);
       lb = max(lb, sv + r[m]);
       tt = sv + pr[m];
+    }
+    if (a.dbg_rec) {
+      uint32_t rp[FrontGeom<M>::HW];
+#pragma unroll
+      for (int h = 0; h < FrontGeom<M>::HW; ++h) {
+        const uint32_t lo = static_cast<uint32_t>(r[2 * h] - a.min_tails[2 * h]);
+        const uint32_t hi = 2 * h + 1 < M ? static_cast<uint32_t>(r[2 * h + 1] - a.min_tails[2 * h + 1]) : 0u;
+        rp[h] = lo | (hi << 16);
+      }
+      front_dbg<M>(a, kind, w, rp, j, lb);
     }
     emit(j, lb);
   }
@@ -206,7 +263,7 @@ __device__ inline int kth_bit(uint32_t x, int k) {
 }
 
 // Child-parallel expansion of n nodes staged in LDS (src[i], with their remain
-// rem[i]): ONE THREAD PER CHILD instead of one per parent. In a narrow window a
+// rem[i]): ONE THREAD PER CHILD instead of one per parent. In a narrow level a
 // thread-per-parent expansion runs its parent's ~20 children one after the other while
 // most lanes idle; here child c finds its parent (binary search on the child offsets)
 // and its job (k-th unscheduled bit), then bounds itself from the parent's front and
@@ -214,16 +271,24 @@ __device__ inline int kth_bit(uint32_t x, int k) {
 // parent's minus its own row). Leaves lower the incumbent and are counted in nleaf;
 // survivors are compacted (block scan) and handed to store(index, child words, child
 // remain). Returns the survivor count. Every thread calls it (block-wide scans).
+// Children of the n staged nodes: their offsets into sm.coff, the total returned.
+template <int M>
+__device__ inline int front_child_offsets(FrontSmem<M>& sm, const uint4 (*src)[FrontGeom<M>::VPN], int n) {
+  int T = 0;
+  const int off = block_exclusive_scan(threadIdx.x < n ? __popc(src[threadIdx.x][0].y) : 0, sm.scan, &T);
+  if (static_cast<int>(threadIdx.x) < n) sm.coff[threadIdx.x] = off;
+  __syncthreads();
+  return T;
+}
+
+// (T children, offsets in sm.coff: front_child_offsets)
 template <int M, class Store>
 __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const uint4 (*src)[FrontGeom<M>::VPN],
-                                      const uint32_t (*rem)[FrontGeom<M>::HW], int n, int best, int& nleaf, Store store) {
+                                      const uint32_t (*rem)[FrontGeom<M>::HW], int n, int T, int best, int& nleaf,
+                                      Store store) {
   using G = FrontGeom<M>;
   constexpr int HW = G::HW;
   const int tid = threadIdx.x;
-  int T = 0;
-  const int off = block_exclusive_scan(tid < n ? __popc(src[tid][0].y) : 0, sm.scan, &T);
-  if (tid < n) sm.coff[tid] = off;
-  __syncthreads();
   int nout = 0;
   for (int cb = 0; cb < T; cb += kBlock) {
     const int c = cb + tid;
@@ -253,14 +318,15 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
       }
       j = kth_bit(w[1], c - sm.coff[lo]);
       const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
-      uint32_t pw[HW];
+      uint32_t pw[HW], rp[HW];
 #pragma unroll
       for (int h = 0; h < HW; ++h) {
         pw[h] = row[h];
-        cr[h] = rem[lo][h] - pw[h];  // the child's remain (packed halves never borrow: row <= remain)
+        rp[h] = rem[lo][h];
+        cr[h] = rp[h] - pw[h];  // the child's remain (packed halves never borrow: row <= remain)
       }
       auto pm = [&](int m) { return static_cast<int>((pw[m >> 1] >> ((m & 1) * 16)) & 0xffffu); };
-      auto rm = [&](int m) { return static_cast<int>((rem[lo][m >> 1] >> ((m & 1) * 16)) & 0xffffu) + a.min_tails[m]; };
+      auto rm = [&](int m) { return static_cast<int>((rp[m >> 1] >> ((m & 1) * 16)) & 0xffffu) + a.min_tails[m]; };
       const int f0 = front_of<M>(w, 0);
       int lb = f0 + rm(0);
       int tt = f0 + pm(0);
@@ -270,6 +336,7 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
         lb = max(lb, sv + rm(m));
         tt = sv + pm(m);
       }
+      if (a.dbg_rec) front_dbg<M>(a, kDbgCp, w, rp, j, lb);
       if (static_cast<int>(w[0] & 0xffu) + 1 == a.jobs) {
         ++nleaf;
         if (lb < best) atomicMin(&a.pool.ctl->best.v, lb);
@@ -289,24 +356,106 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
   return nout;
 }
 
-// Two-level chunk, child-parallel (default): the chunk's v.bp parents go to LDS, their
-// children are expanded one per thread into sm.mid, then the survivors' children one
-// per thread into the chunk's slot region. Same counts as front_two_level: level-1
-// survivors expanded here are pushed-and-expanded tree nodes (high half of the leaf
-// word); level-1 survivors beyond sm.mid's kBlock nodes go out unexpanded (first in the
-// slot region) with the level-2 survivors as the chunk's output.
+// Thread-per-node expansion of n <= kBlock nodes staged in LDS with their carried
+// remains: thread i bounds all children of node i in turn (the chain of front_parent,
+// without its pass over the unscheduled rows), then the survivors are compacted (block
+// scan) and handed to store(index, child words, child remain). Wider levels take this
+// path: fewer instructions per child than front_expand_cp (no parent search, one node
+// load per parent), and the serial loop is short once most lanes hold a node.
+template <int M, class Store>
+__device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm,
+                                      const uint4 (*src)[FrontGeom<M>::VPN], const uint32_t (*rem)[FrontGeom<M>::HW],
+                                      int n, int best, int& nleaf, Store store) {
+  using G = FrontGeom<M>;
+  constexpr int HW = G::HW;
+  const int tid = threadIdx.x;
+  uint32_t w[G::NW], rp[HW];
+#pragma unroll
+  for (int i = 0; i < G::NW; ++i) w[i] = 0;
+#pragma unroll
+  for (int h = 0; h < HW; ++h) rp[h] = 0;
+  if (tid < n) {
+#pragma unroll
+    for (int q = 0; q < G::VPN; ++q) {
+      const uint4 x = src[tid][q];
+      w[4 * q] = x.x;
+      w[4 * q + 1] = x.y;
+      w[4 * q + 2] = x.z;
+      w[4 * q + 3] = x.w;
+    }
+#pragma unroll
+    for (int h = 0; h < HW; ++h) rp[h] = rem[tid][h];
+  }
+  uint32_t surv = 0;
+  int nsurv = 0;
+  const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
+  {
+    int f[M], r[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      f[m] = front_of<M>(w, m);
+      r[m] = static_cast<int>((rp[m >> 1] >> ((m & 1) * 16)) & 0xffffu) + a.min_tails[m];
+    }
+    for (uint32_t x = w[1]; x; x &= x - 1) {
+      const int j = __builtin_ctz(x);
+      int pr[M];
+      front_row<M>(sm.ptab[j], pr);
+      int lb = f[0] + r[0];
+      int tt = f[0] + pr[0];
+#pragma unroll
+      for (int m = 1; m < M; ++m) {
+        const int sv = max(tt, f[m]);
+        lb = max(lb, sv + r[m]);
+        tt = sv + pr[m];
+      }
+      if (a.dbg_rec) front_dbg<M>(a, kDbgTp, w, rp, j, lb);
+      if (leaf) {
+        ++nleaf;
+        if (lb < best) atomicMin(&a.pool.ctl->best.v, lb);
+      } else if (lb < best) {
+        ++nsurv;
+        surv |= 1u << j;
+      }
+    }
+  }
+  int tot = 0;
+  int idx = block_exclusive_scan(nsurv, sm.scan, &tot);
+  while (surv) {
+    const int j = __builtin_ctz(surv);
+    surv &= surv - 1;
+    uint32_t cw[G::NW], cr[HW];
+    front_child<M>(sm, w, j, cw);
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
+#pragma unroll
+    for (int h = 0; h < HW; ++h) cr[h] = rp[h] - row[h];
+    store(idx++, cw, cr);
+  }
+  return tot;
+}
+
+// Multi-level chunk (fused iterations): the chunk's v.bp parents go to LDS with their
+// remains, then up to v.levels tree levels are expanded in place — each level's
+// survivors become the next level's nodes in the other LDS buffer (at most CAP of them;
+// the rest go out unexpanded, first in the slot region), and the last level's survivors
+// go out. A level of at most a.cp_max children is expanded child-parallel (passes of
+// kBlock children), a wider one thread-per-node. Counts: nodes staged and expanded here are pushed-and-expanded tree
+// nodes (high half of the leaf word); everything that goes out is the chunk's output.
+// One dependent kernel covers up to 4 tree levels of a narrow window (ref: one kernel
+// per level, pfsp_multigpu_cuda.c:221-332).
 template <int M>
-__device__ inline void front_two_level_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t,
-                                          int best) {
+__device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t,
+                                         int best) {
   using G = FrontGeom<M>;
   using Node = PfspFrontNode<M>;
-  static_assert(G::BPF_CP * (G::NJ - 1) + G::MID * (G::NJ - 1) <= G::SLOT, "chunk output must fit its slot region");
-  static_assert(G::MID <= kBlock && G::BPF_CP <= kBlock, "one thread per staged node");
+  static_assert(G::BPF_CP * (G::NJ - 1) + (G::LMAX - 1) * G::CAP * (G::NJ - 1) <= G::SLOT,
+                "chunk output must fit its slot region");
+  static_assert(G::CAP <= kBlock && G::BPF_CP <= G::CAP, "one thread per staged node");
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  const int L = min(v.levels, G::LMAX);
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 g0 = static_cast<u64>(ch) * v.bp;
     const int n0 = static_cast<int>(min(static_cast<u64>(v.bp), v.B - g0));
@@ -315,7 +464,7 @@ __device__ inline void front_two_level_cp(const PfspFrontArgs<M>& a, FrontSmem<M
       // < 65536, pfsp_front_ok), by the thread that stages it
       uint32_t w[G::NW];
       front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
-      front_store<M>(&sm.par[tid][0], w);
+      front_store<M>(&sm.lvl[0][tid][0], w);
       uint32_t r2[G::HW];
 #pragma unroll
       for (int h = 0; h < G::HW; ++h) r2[h] = 0;
@@ -325,35 +474,45 @@ __device__ inline void front_two_level_cp(const PfspFrontArgs<M>& a, FrontSmem<M
         for (int h = 0; h < G::HW; ++h) r2[h] += row[h];
       }
 #pragma unroll
-      for (int h = 0; h < G::HW; ++h) sm.rpar[tid][h] = r2[h];
+      for (int h = 0; h < G::HW; ++h) sm.rlv[0][tid][h] = r2[h];
     }
     __syncthreads();
-    int nleaf = 0;
+    const bool first = ch == static_cast<int>(blockIdx.x);
+    if (first) front_stamp(a, 3);
+    int nleaf = 0, inner = 0, o = 0, n = n0, cur = 0;
     uint4* const out = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
-    const int n1 = front_expand_cp<M>(a, sm, sm.par, sm.rpar, n0, best, nleaf,
-                                      [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {
-                                        if (i < G::MID) {
-                                          front_store<M>(&sm.mid[i][0], c);
+    for (int lev = 0; lev < L && n > 0; ++lev) {
+      const bool last = lev == L - 1;
+      const int nx = cur ^ 1;
+      auto store = [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {
+        if (!last && i < G::CAP) {
+          front_store<M>(&sm.lvl[nx][i][0], c);
 #pragma unroll
-                                          for (int h = 0; h < G::HW; ++h) sm.rmid[i][h] = r[h];
-                                        } else {
-                                          front_store<M>(out + (i - G::MID) * G::VPN, c);  // out unexpanded
-                                        }
-                                      });
-    __syncthreads();  // level-1 survivors visible
-    const int n1e = min(n1, G::MID), ovf = n1 - n1e;
-    const int n2 = front_expand_cp<M>(a, sm, sm.mid, sm.rmid, n1e, best, nleaf,
-                                      [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&)[G::HW]) {
-                                        front_store<M>(out + (ovf + i) * G::VPN, c);
-                                      });
+          for (int h = 0; h < G::HW; ++h) sm.rlv[nx][i][h] = r[h];
+        } else {
+          front_store<M>(out + (o + (last ? i : i - G::CAP)) * G::VPN, c);
+        }
+      };
+      const int T = front_child_offsets<M>(sm, sm.lvl[cur], n);
+      const int nn = T > a.cp_max ? front_expand_tp<M>(a, sm, sm.lvl[cur], sm.rlv[cur], n, best, nleaf, store)
+                                  : front_expand_cp<M>(a, sm, sm.lvl[cur], sm.rlv[cur], n, T, best, nleaf, store);
+      __syncthreads();  // the next level is visible; this level's buffer is free
+      o += last ? nn : max(0, nn - G::CAP);
+      n = last ? 0 : min(nn, G::CAP);
+      inner += n;
+      cur = nx;
+      if (first) front_stamp(a, 4 + lev);
+    }
     int leaves = 0;
     (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
     if (tid == 0) {
-      cnt_out[ch] = ovf + n2;
-      lcnt_out[ch] = leaves | (n1e << 16);
+      cnt_out[ch] = o;
+      lcnt_out[ch] = leaves | (inner << 16);
     }
-    __syncthreads();  // sm.par / sm.mid / sm.coff are rewritten by the next chunk
+    __syncthreads();  // sm.lvl / sm.coff are rewritten by the next chunk
+    if (first) front_stamp(a, 8);
   }
+  front_stamp(a, 15);
 }
 
 // Local DFS chunk loop (v.local): chunk ch takes v.bp window parents, then keeps
@@ -391,15 +550,18 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
       uint32_t surv = 0;
       int nsurv = 0;
       const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-      front_parent<M>(a, sm, w, [&](int j, int lb) {
-        if (leaf) {
-          ++nleaf;
-          if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-        } else if (lb < best) {
-          ++nsurv;
-          surv |= 1u << j;
-        }
-      });
+      front_parent<M>(
+          a, sm, w,
+          [&](int j, int lb) {
+            if (leaf) {
+              ++nleaf;
+              if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+            } else if (lb < best) {
+              ++nsurv;
+              surv |= 1u << j;
+            }
+          },
+          kDbgLocal);
       int tot = 0;
       const int off = block_exclusive_scan(nsurv, sm.scan, &tot);
       front_emit<M>(sm, w, surv, reinterpret_cast<uint4*>(stk + top + off));
@@ -424,17 +586,18 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
 //
 // Occupancy: the iterations are latency-bound (the per-child chain, LDS row reads), so
 // the register budget is capped for more resident waves: 6 per SIMD up to 10 machines,
-// 4 for 20 (f, remain and a p row stay in registers without scratch).
-// (8 waves per SIMD for M <= 10, SGPRs spilled to VGPR lanes, measured: ta014 +2 %,
-// ta008 -4 %; not kept, profiles/r3/probes/front_w8_ab.txt)
+// 4 for 20 (f, remain and a p row stay in registers without scratch); FrontGeom::WAVES
+// sizes the engine's grid to match. (Compiled for 7 — 94 SGPRs, 72 spilled to VGPR
+// lanes — the headline was 3 % slower than at 6.)
 template <int M>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 10 ? 6 : 4)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FrontGeom<M>::WAVES)))
 void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
   using G = FrontGeom<M>;
   using Node = PfspFrontNode<M>;
   __shared__ FrontSmem<M> sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
+  front_stamp(a, 0);
   // p table loads issued together with pool_begin's (one memory round trip)
   constexpr int PTN = (G::NJ * G::MS + kBlock - 1) / kBlock;
   uint16_t ptv[PTN];
@@ -443,7 +606,8 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     const int x = tid + i * kBlock;
     ptv[i] = x < a.jobs * G::MS ? a.ptab[x] : 0;
   }
-  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, a.bpf, G::LT, G::NJ * (G::NJ - 1));
+  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, a.bpf, G::LT, G::NJ * (G::NJ - 1), G::LMAX);
+  front_stamp(a, 1);
   if (v.B == 0 || v.overflow) return;
   {
     uint16_t* pt = &sm.ptab[0][0];
@@ -457,12 +621,13 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
   pool_spill_leftovers<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, sm.pool);
   __syncthreads();
+  front_stamp(a, 2);
   if (v.local) {
     front_local<M>(a, sm, v, t, best);
     return;
   }
   if (v.fused) {
-    front_two_level_cp<M>(a, sm, v, t, best);
+    front_multi_level<M>(a, sm, v, t, best);
     return;
   }
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
@@ -471,6 +636,7 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
 #pragma unroll
     for (int i = 0; i < G::NW; ++i) w[i] = 0;
     if (gi < v.B) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
+    const bool first = ch == static_cast<int>(blockIdx.x);
     const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
     // children this rank keeps (all of them outside the split iteration)
     uint32_t kmask = ~0u;
@@ -483,16 +649,20 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     }
     uint32_t surv = 0;
     int nsurv = 0, nleaf = 0;
-    front_parent<M>(a, sm, w, [&](int j, int lb) {
-      const bool keep = (kmask >> j) & 1u;
-      if (leaf) {
-        nleaf += keep;
-        if (lb < best) atomicMin(&pa.ctl->best.v, lb);
-      } else if (keep && lb < best) {
-        ++nsurv;
-        surv |= 1u << j;
-      }
-    });
+    front_parent<M>(
+        a, sm, w,
+        [&](int j, int lb) {
+          const bool keep = (kmask >> j) & 1u;
+          if (leaf) {
+            nleaf += keep;
+            if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+          } else if (keep && lb < best) {
+            ++nsurv;
+            surv |= 1u << j;
+          }
+        },
+        v.split ? kDbgSplit : kDbgOne);
+    if (first) front_stamp(a, 4);
     // one scan for both counts: survivors (<= 256 x 19) in bits 0-12, leaves (<= 256)
     // in bits 13-21
     int tot = 0;
@@ -501,8 +671,11 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
       cnt_out[ch] = tot & 0x1fff;
       lcnt_out[ch] = (tot >> 13) & 0x1ff;
     }
+    if (first) front_stamp(a, 5);
     front_emit<M>(sm, w, surv, reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off));
+    if (first) front_stamp(a, 6);
   }
+  front_stamp(a, 15);
 }
 
 // Reference-style evaluation for the tests (ref evaluate_gpu, PFSP_gpu_lib.cu:129-152):

@@ -81,6 +81,11 @@ struct PoolArgs {
   int fuse_max;     // two-level iterations for windows of at most this many parents (0: off)
   int local_steps;  // > 1: local DFS iterations of up to this many steps per chunk (kernels that have them)
   int local_min;    // wide local DFS when the pool holds at least this many parents (0: 4 grid windows)
+  // multi-level iterations (kernels with LMAX > 2): a fused window of at most deep_per[0]
+  // parents per workgroup is expanded 3 levels deep, of at most deep_per[1] 4 levels deep
+  // (capped by deep_levels); 2 levels otherwise
+  int deep_levels;
+  int deep_per[2];
 };
 
 // Per-chunk leaf word: leaves in the low 16 bits; the high 16 bits count the
@@ -133,7 +138,8 @@ struct IterView {
   int nch_in, nchunks;
   bool overflow;
   bool split;         // this iteration splits the (replicated) pool between ranks
-  bool fused;         // two-level iteration: chunks of BPF parents, grandchildren out
+  bool fused;         // multi-level iteration: chunks of BPF parents, `levels` tree levels deep
+  int levels;         // fused iterations: tree levels expanded per chunk (2..LMAX)
   bool local;         // local DFS iteration: each chunk steps on its own stack
   int bp;             // window parents per chunk
   int steps;          // local DFS: steps per chunk at most
@@ -170,7 +176,7 @@ template <class Node, int MAXCHUNKS>
 // levels; what is left on the stack is the chunk's output. Several tree levels per
 // dependent kernel, and the next iteration re-deals the stacks over the grid.
 __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, PoolSmem<MAXCHUNKS>& ps,
-                                      int BPF = 0, int LT = 1, int GROW2 = 0) {
+                                      int BPF = 0, int LT = 1, int GROW2 = 0, int LMAX = 2) {
   const int s_in = t % 3, s_out = (t + 1) % 3;
   const int b_in = t & 1;
   PoolCtl* ctl = pa.ctl;
@@ -192,6 +198,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     v.C = v.B = v.nb = v.ns = v.L = v.Snew = v.bot = 0;
     v.nchunks = 0;
     v.overflow = v.split = v.fused = v.local = v.armed = false;
+    v.levels = 1;
     v.bp = BP;
     v.steps = v.cap = 0;
     v.srank = v.sworld = 0;
@@ -216,7 +223,9 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // for the ramp-up and the tail measured slower and was removed: profiles/r2/.)
   const u64 full = static_cast<u64>(gridDim.x) * BP;
   const u64 lmin = pa.local_min > 0 ? static_cast<u64>(pa.local_min) : 4 * full;
-  v.local = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= max(lmin, full);
+  // (an explicit pa.local_min may be below one grid window: wide BFS levels of a small
+  // tree then also take a few local steps per dependent kernel)
+  v.local = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= (pa.local_min > 0 ? lmin : max(lmin, full));
   v.steps = pa.local_steps;
   v.cap = 0x7fffffff;
   if (v.local) v.B = min(v.B, full);
@@ -237,6 +246,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   v.fused = !v.local && BPF > 0 && (!armed || fuse_armed) &&
             v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
   int bp = BP;
+  v.levels = v.fused ? 2 : 1;
   if (v.fused) {
     // up to BPF parents per two-level chunk, fewer when the window is narrower than the
     // grid: more workgroups share a narrow window (each with fewer serial passes). While
@@ -244,6 +254,11 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     // same frontier by position), so those chunks keep BPF parents.
     const u64 per = (v.B + gridDim.x - 1) / gridDim.x;
     bp = armed ? BPF : static_cast<int>(min(static_cast<u64>(BPF), max(per, 1ull)));
+    // narrower windows go deeper: 3 or 4 levels per dependent kernel while a chunk's
+    // levels stay in LDS (never while armed: the split must see the replicated levels)
+    const int lmax = min(LMAX, pa.deep_levels);
+    if (!armed && lmax >= 3 && per <= static_cast<u64>(pa.deep_per[0])) v.levels = 3;
+    if (!armed && lmax >= 4 && per <= static_cast<u64>(pa.deep_per[1])) v.levels = 4;
   }
   if (v.local) {
     // spread a window smaller than the grid over every workgroup

@@ -1,0 +1,221 @@
+// Native RCCL transport of the one-process-per-GPU runtime.
+//
+// Ref pfsp_dist_multigpu_cuda.c:122-137,364-469: the comm thread moves donated nodes
+// with MPI_Allgather(sizes) + MPI_Allgatherv(nodes), every rank receiving every
+// donor's block through host memory. Here one RCCL communicator per process (one GPU
+// per rank, over xGMI) carries targeted donor -> receiver pairs only:
+//   engine.export_device (pool bottom -> device staging, compute stream; the transfer
+//   stream waits for it) -> ncclGroupStart, ncclSend / ncclRecv on the engine's
+//   transfer stream, ncclGroupEnd -> engine.import_device (the compute stream waits for
+//   the transfer stream, then appends) — stream-ordered, no host wait, no Python.
+// The communicator is built from an ncclUniqueId that rank 0 creates and the caller
+// distributes (parallel/comm.py: one broadcast over the process group). The library is
+// the librccl.so.1 that torch has already loaded (same SONAME): one RCCL per process.
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../core/dist_rounds.hpp"
+#include "../core/engine_api.hpp"
+#include "device_common.hpp"
+
+#define TTS_NCCL_CHECK(expr)                                                                               \
+  do {                                                                                                     \
+    ncclResult_t _r = (expr);                                                                              \
+    if (_r != ncclSuccess)                                                                                 \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(_r) + " at " + __FILE__ + ":" + \
+                               std::to_string(__LINE__) + " in " #expr);                                   \
+  } while (0)
+
+namespace tts {
+
+class RcclTransport {
+ public:
+  static std::vector<uint8_t> new_id() {
+    ncclUniqueId id;
+    TTS_NCCL_CHECK(ncclGetUniqueId(&id));
+    return std::vector<uint8_t>(reinterpret_cast<uint8_t*>(&id), reinterpret_cast<uint8_t*>(&id) + sizeof(id));
+  }
+
+  RcclTransport(const std::vector<uint8_t>& id, int rank, int world, int device)
+      : rank_(rank), world_(world), device_(device) {
+    if (id.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("RcclTransport: bad unique id size");
+    if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("RcclTransport: bad rank/world");
+    ncclUniqueId uid;
+    std::memcpy(&uid, id.data(), sizeof(uid));
+    TTS_HIP_CHECK(hipSetDevice(device_));
+    TTS_NCCL_CHECK(ncclCommInitRank(&comm_, world, uid, rank));
+  }
+  ~RcclTransport() {
+    (void)hipSetDevice(device_);
+    for (int b = 0; b < 2; ++b)
+      if (buf_[b]) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(buf_[b]);
+      }
+    if (comm_) (void)ncclCommDestroy(comm_);
+  }
+  RcclTransport(const RcclTransport&) = delete;
+  RcclTransport& operator=(const RcclTransport&) = delete;
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  int device() const { return device_; }
+  unsigned long long transfers() const { return transfers_; }
+  unsigned long long bytes_sent() const { return bytes_sent_; }
+  unsigned long long bytes_recv() const { return bytes_recv_; }
+
+  // The plan's transfers that concern this rank (every rank calls this with the same
+  // plan, in the same round); returns (nodes sent, nodes received).
+  std::pair<size_t, size_t> execute(const Plan& plan, IEngine& e) {
+    size_t nout = 0, nin = 0;
+    const std::vector<P2PCall> calls = p2p_calls(plan, rank_, &nout, &nin);
+    if (calls.empty()) return {0, 0};
+    if (e.device() != device_) throw std::invalid_argument("RcclTransport: engine on another device");
+    TTS_HIP_CHECK(hipSetDevice(device_));
+    const size_t nb = e.node_bytes();
+    hipStream_t xs = reinterpret_cast<hipStream_t>(e.transfer_stream());
+    if (!xs) throw std::invalid_argument("RcclTransport: engine has no transfer stream (GPU engines only)");
+    uint8_t* out = static_cast<uint8_t*>(staging(0, nout * nb, xs));
+    uint8_t* in = static_cast<uint8_t*>(staging(1, nin * nb, xs));
+    if (nout) {
+      const size_t got = e.export_device(out, nout);
+      if (got != nout)
+        throw std::runtime_error("rank " + std::to_string(rank_) + ": planned to send " + std::to_string(nout) +
+                                 " nodes, the pool gave " + std::to_string(got));
+    }
+    TTS_NCCL_CHECK(ncclGroupStart());
+    for (const P2PCall& c : calls) {
+      if (c.send)
+        TTS_NCCL_CHECK(ncclSend(out + c.offset * nb, c.count * nb, ncclUint8, c.peer, comm_, xs));
+      else
+        TTS_NCCL_CHECK(ncclRecv(in + c.offset * nb, c.count * nb, ncclUint8, c.peer, comm_, xs));
+    }
+    TTS_NCCL_CHECK(ncclGroupEnd());
+    if (nin) e.import_device(in, nin);
+    ++transfers_;
+    bytes_sent_ += nout * nb;
+    bytes_recv_ += nin * nb;
+    return {nout, nin};
+  }
+
+  // World-1 check of the whole path on one GPU: n nodes go pool -> staging -> RCCL send
+  // to self / receive from self -> staging -> pool. Returns the nodes moved.
+  size_t self_loop(IEngine& e, size_t n) {
+    TTS_HIP_CHECK(hipSetDevice(device_));
+    const size_t nb = e.node_bytes();
+    hipStream_t xs = reinterpret_cast<hipStream_t>(e.transfer_stream());
+    if (!xs) throw std::invalid_argument("RcclTransport: GPU engines only");
+    uint8_t* out = static_cast<uint8_t*>(staging(0, n * nb, xs));
+    uint8_t* in = static_cast<uint8_t*>(staging(1, n * nb, xs));
+    const size_t got = e.export_device(out, n);
+    if (got == 0) return 0;
+    TTS_NCCL_CHECK(ncclGroupStart());
+    TTS_NCCL_CHECK(ncclSend(out, got * nb, ncclUint8, rank_, comm_, xs));
+    TTS_NCCL_CHECK(ncclRecv(in, got * nb, ncclUint8, rank_, comm_, xs));
+    TTS_NCCL_CHECK(ncclGroupEnd());
+    e.import_device(in, got);
+    return got;
+  }
+
+  // Every rank sends a rank-stamped pattern of `bytes` to every peer and checks what it
+  // receives word by word (the node-transfer path, before any solve relies on it).
+  // `corrupt` flips one received word (fault injection). Returns {peers, seconds}.
+  std::pair<int, double> preflight(size_t bytes, bool corrupt = false) {
+    TTS_HIP_CHECK(hipSetDevice(device_));
+    const size_t words = std::max<size_t>(1, bytes / 4);
+    std::vector<int> peers;
+    for (int p = 0; p < world_; ++p)
+      if (p != rank_) peers.push_back(p);
+    if (peers.empty()) return {0, 0.0};
+    hipStream_t s = nullptr;
+    TTS_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const size_t np = peers.size();
+    std::vector<uint32_t> src(np * words), got(np * words, 0);
+    auto pat = [](size_t i, int from, int to) {
+      return static_cast<uint32_t>((i * 2654435761ull + static_cast<unsigned>(from) * 0x9E3779B1u +
+                                    static_cast<unsigned>(to) * 0x85EBCA77u + 12345u) & 0x7fffffffu);
+    };
+    for (size_t k = 0; k < np; ++k)
+      for (size_t i = 0; i < words; ++i) src[k * words + i] = pat(i, rank_, peers[k]);
+    uint32_t *dsrc = nullptr, *ddst = nullptr;
+    TTS_HIP_CHECK(hipMalloc(&dsrc, src.size() * 4));
+    TTS_HIP_CHECK(hipMalloc(&ddst, got.size() * 4));
+    TTS_HIP_CHECK(hipMemcpy(dsrc, src.data(), src.size() * 4, hipMemcpyHostToDevice));
+    TTS_HIP_CHECK(hipMemset(ddst, 0, got.size() * 4));
+    hipEvent_t e0, e1;
+    TTS_HIP_CHECK(hipEventCreate(&e0));
+    TTS_HIP_CHECK(hipEventCreate(&e1));
+    TTS_HIP_CHECK(hipEventRecord(e0, s));
+    std::string err;
+    try {
+      TTS_NCCL_CHECK(ncclGroupStart());
+      for (size_t k = 0; k < np; ++k) {
+        TTS_NCCL_CHECK(ncclSend(dsrc + k * words, words * 4, ncclUint8, peers[k], comm_, s));
+        TTS_NCCL_CHECK(ncclRecv(ddst + k * words, words * 4, ncclUint8, peers[k], comm_, s));
+      }
+      TTS_NCCL_CHECK(ncclGroupEnd());
+      TTS_HIP_CHECK(hipEventRecord(e1, s));
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+      TTS_HIP_CHECK(hipMemcpy(got.data(), ddst, got.size() * 4, hipMemcpyDeviceToHost));
+    } catch (const std::exception& x) {
+      err = x.what();
+    }
+    float ms = 0;
+    if (err.empty()) (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(dsrc);
+    (void)hipFree(ddst);
+    (void)hipStreamDestroy(s);
+    if (!err.empty())
+      throw std::runtime_error("rank " + std::to_string(rank_) + ": RCCL point-to-point preflight failed (" +
+                               std::to_string(np) + " peers): " + err);
+    if (corrupt) got[0] ^= 1u;
+    std::string bad;
+    for (size_t k = 0; k < np; ++k)
+      for (size_t i = 0; i < words; ++i)
+        if (got[k * words + i] != pat(i, peers[k], rank_)) {
+          bad += (bad.empty() ? "" : ",") + std::to_string(peers[k]);
+          break;
+        }
+    if (!bad.empty())
+      throw std::runtime_error("rank " + std::to_string(rank_) + ": RCCL preflight: data received from rank(s) " +
+                               bad + " does not match what they sent; node transfers would corrupt the pools");
+    return {static_cast<int>(np), ms * 1e-3};
+  }
+
+ private:
+  // Staging block `which` (0 out, 1 in) of at least `bytes`; a grown block replaces the
+  // old one only after the transfer stream has drained (an RCCL op may still read it).
+  void* staging(int which, size_t bytes, hipStream_t xs) {
+    if (bytes == 0) return buf_[which];
+    if (cap_[which] < bytes) {
+      if (buf_[which]) {
+        TTS_HIP_CHECK(hipStreamSynchronize(xs));
+        TTS_HIP_CHECK(hipFree(buf_[which]));
+        buf_[which] = nullptr;
+      }
+      size_t c = std::max<size_t>(size_t(64) << 20, cap_[which]);
+      while (c < bytes) c *= 2;
+      TTS_HIP_CHECK(hipMalloc(&buf_[which], c));
+      cap_[which] = c;
+    }
+    return buf_[which];
+  }
+
+  ncclComm_t comm_ = nullptr;
+  int rank_, world_, device_;
+  void* buf_[2] = {nullptr, nullptr};
+  size_t cap_[2] = {0, 0};
+  unsigned long long transfers_ = 0, bytes_sent_ = 0, bytes_recv_ = 0;
+};
+
+}  // namespace tts

@@ -35,6 +35,9 @@ CXX = os.environ.get("CXX_HOST", "g++")
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wno-maybe-uninitialized", "-Wno-unused-function"]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIP_LIBS = [f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
+# the Python module also links librccl.so.1 (csrc/hip/rccl_transport.hpp): a process
+# that imported torch first already holds torch's copy (same SONAME), so one RCCL per process
+HIP_MODULE_LIBS = [*HIP_LIBS, "-lrccl"]
 HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
@@ -130,7 +133,7 @@ def build_hip(newest: float, jobs: int) -> Path:
         _run([HIPCC, *HIPFLAGS, "-x", "hip", *_py_includes(), "-c", str(CSRC / "bindings" / "py_hip.cpp"), "-o",
               str(bind_o)])
     if _stale(out, newest):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(bind_o), *map(str, objs), *HIP_LIBS, "-o",
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(bind_o), *map(str, objs), *HIP_MODULE_LIBS, "-o",
               str(out)])
     return out
 

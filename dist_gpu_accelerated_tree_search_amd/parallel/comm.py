@@ -8,12 +8,18 @@ transfer issued by all ranks in the same order:
   * status round      one all_gather of a small int64 record per rank
                       (pool size, incumbent, idle flag) — replaces the separate
                       Allreduce(best) + Allgather(termination) + Allgather(needs)
-  * work transfer     batch_isend_irecv donor -> needy only, straight from the
-                      device pool (engine.export_to) into the peer's pool over xGMI;
-                      never an all-gather of everybody's nodes. Stream-ordered:
-                      the copy out of the pool, the RCCL send/recv (on the
-                      engine's transfer stream) and the copy into the peer's pool
-                      are chained with events, without a host wait.
+  * work transfer     donor -> needy only, straight from the device pool into the
+                      peer's pool over xGMI; never an all-gather of everybody's
+                      nodes. With GPU engines the transfer is NATIVE: one RCCL
+                      communicator of this job (csrc/hip/rccl_transport.hpp, built
+                      from a unique id rank 0 broadcasts once) issues ncclGroupStart /
+                      ncclSend / ncclRecv / ncclGroupEnd on the engine's transfer
+                      stream from inside the native round loop — no Python, no torch
+                      tensors per round. Stream-ordered: the copy out of the pool,
+                      the send/recv and the copy into the peer's pool are chained
+                      with events, without a host wait. (TTS_NATIVE_RCCL=0: the same
+                      plan through torch batch_isend_irecv; gloo / CPU engines:
+                      host arrays.)
   * final reduction   all_reduce SUM of counters / MIN of the incumbent.
 When every rank is on this node (torchrun --nnodes=1) the status records, barriers
 and final reductions go through a shared-memory control plane instead
@@ -100,6 +106,7 @@ class Comm:
             self.ctl = self._open_shm_control()
         self.preflight = None
         self.p2p_ok = True
+        self.rccl = None  # native RCCL transport (GPU ranks over nccl)
         # fault injection (like TTS_FAULT_*): the preflight runs on any backend and the
         # data this rank receives is corrupted
         fault = os.environ.get("TTS_FAULT_P2P_RANK")
@@ -107,7 +114,13 @@ class Comm:
             try:
                 if use_gpu and self.backend == "nccl":
                     self._connect_peers()
-                if fault not in (None, "") and int(fault) == self.rank:
+                    if os.environ.get("TTS_NATIVE_RCCL", "1") != "0":
+                        self.rccl = self._open_rccl()
+                if self.rccl is not None:
+                    # the native path end to end (what the round loop will use)
+                    self.preflight = self.rccl.preflight(
+                        4 << 20, corrupt=fault not in (None, "") and int(fault) == self.rank)
+                elif fault not in (None, "") and int(fault) == self.rank:
                     real = self._p2p
 
                     def corrupt(outgoing, incoming, src, dst, nb):
@@ -189,6 +202,27 @@ class Comm:
                                "backend would corrupt the pools")
         return {"ok": True, "peers": len(peers), "bytes_per_peer": words * 4, "seconds": dt,
                 "GBps": len(peers) * words * 4 / max(dt, 1e-9) / 1e9}
+
+    def _open_rccl(self):
+        """This job's native RCCL communicator: rank 0 creates the unique id, one
+        broadcast over the process group hands it to every rank, every rank builds
+        its communicator (ncclCommInitRank waits for all of them)."""
+        from .. import ops
+
+        torch, dist = self.torch, self.dist
+        H = ops.hip()
+        uid = H.RcclTransport.new_id() if self.rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=self.device)
+        dist.broadcast(t, src=0)
+        uid = bytes(t.cpu().tolist())
+        return H.RcclTransport(uid, self.rank, self.world, self.device.index)
+
+    def transport(self, engine, node_bytes: int):
+        """What the native round loop moves nodes with: the native RCCL transport for a
+        GPU engine (no callback into Python), else execute_transfers."""
+        if self.rccl is not None and int(getattr(engine, "transfer_stream", 0) or 0):
+            return self.rccl
+        return lambda plan: self.execute_transfers(plan, engine, node_bytes)
 
     def _connect_peers(self) -> None:
         """RCCL sets up a point-to-point channel on first use; do it for every pair now
@@ -283,6 +317,7 @@ class Comm:
 
     def close(self) -> None:
         self.ctl = None
+        self.rccl = None
         if self._owns_pg and self.dist.is_initialized():
             self.dist.destroy_process_group()
             self._owns_pg = False
@@ -346,6 +381,12 @@ class Comm:
         incoming = [(d, k) for (d, r, k) in plan if r == me and k > 0]
         if not outgoing and not incoming:
             return 0, 0
+        if self.rccl is not None and int(getattr(engine, "transfer_stream", 0) or 0):
+            sent, got = self.rccl.execute([tuple(t) for t in plan], engine)
+            self.device_transfers += 1
+            self.bytes_sent += sent * node_bytes
+            self.bytes_recv += got * node_bytes
+            return sent, got
         total_out = sum(k for _, k in outgoing)
         total_in = sum(k for _, k in incoming)
         torch, dist = self.torch, self.dist

@@ -246,7 +246,9 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, t_start: float, t_init: 
     mod = ops.hip() if native == "_tts_hip" else ops.cpu()
     t_loop = time.perf_counter()
     shm = comm.control_address(mod)
-    out = mod.dist_rounds(engine, shm, None if shm else comm.allgather_i64, rank, world, opts, transfer,
+    # GPU ranks over RCCL: the native transport, no Python in the loop
+    xfer = comm.transport(engine, model.node_bytes) if comm.rccl is not None else transfer
+    out = mod.dist_rounds(engine, shm, None if shm else comm.allgather_i64, rank, world, opts, xfer,
                           hook if cfg.checkpoint_dir else None, int(rounds0), float(comm.timeout_s))
     t_search = time.perf_counter() - t_loop
     cnt, tms = out["counts"], out["times"]
@@ -330,8 +332,9 @@ class DistSolver:
         # (init_per_rank nodes); without it, a host BFS to world * init_per_rank nodes
         # and the round-robin share (ref roundRobin_distribution)
         warm = cfg.init_per_rank if split else world * cfg.init_per_rank
+        self._xfer = comm.transport(engine, model.node_bytes)  # kept alive with the session
         self._s = mod.DistSession(engine, model, shm, None if shm else comm.allgather_i64, comm.rank, world, opts,
-                                  lambda plan: comm.execute_transfers(plan, engine, model.node_bytes), None,
+                                  self._xfer, None,
                                   int(warm), int(cfg.split_per_rank * world), float(comm.timeout_s), bool(split))
 
     def solve_raw(self, ub: int = 1) -> tuple:
