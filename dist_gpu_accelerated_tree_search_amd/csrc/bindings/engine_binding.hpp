@@ -43,6 +43,8 @@ inline py::dict engine_stats_dict(const EngineStats& s) {
   d["host_nodes"] = s.host_nodes;
   d["capacity"] = s.capacity;
   d["exports"] = s.exports;
+  d["left_inflight"] = s.left_inflight;
+  d["overlapped_exports"] = s.overlapped_exports;
   d["imports"] = s.imports;
   d["pinned_bytes"] = s.pinned_bytes;
   d["cpu_tree"] = s.cpu_tree;
@@ -212,6 +214,7 @@ inline DistOptions dist_options_from(const py::dict& o) {
   get("max_rounds", opt.max_rounds);
   get("time_limit", opt.time_limit);
   get("live_best", opt.live_best);
+  get("overlap", opt.overlap);
   get("checkpoint_every", opt.checkpoint_every);
   get("watchdog_s", opt.watchdog_s);
   get("watchdog_abort", opt.watchdog_abort);
@@ -288,6 +291,7 @@ inline py::dict outcome_dict(const DistOutcome& out) {
   d["counts"] = iv;  // tree sol sent received transfers_in transfers_out steals success_steals idle_rounds
                      // early_rounds dropped cpu_tree cpu_sol (CPU-worker share of a hybrid rank)
   d["times"] = fv;   // t_run t_comm t_idle t_termination t_load_bal t_memcpy t_malloc
+  d["overlapped_rounds"] = out.overlapped_rounds;  // rounds with a replay in flight, per rank
   return d;
 }
 

@@ -195,6 +195,7 @@ struct DistOptions {
   double time_limit = 0;                          // stop at the first round after this many seconds
                                                   // on any rank (0: never; throughput time boxes)
   bool live_best = true;                          // exchange the incumbent after every replay (board)
+  bool overlap = true;                            // rounds overlap a running replay (IEngine::set_overlap)
   long checkpoint_every = 0;                      // RoundHook every k rounds (0: never)
   double watchdog_s = 0;                          // report a phase longer than this
   bool watchdog_abort = false;
@@ -212,6 +213,8 @@ struct DistOutcome {
   std::vector<unsigned long long> tree, sol, sent, received, transfers_in, transfers_out, steals, success_steals,
       idle_rounds, early_rounds, dropped, cpu_tree, cpu_sol;
   std::vector<double> t_run, t_comm, t_idle, t_termination, t_load_bal, t_memcpy, t_malloc;
+  // rounds this rank spent with a replay in flight (the GPU searching during the round)
+  std::vector<unsigned long long> overlapped_rounds;
   unsigned long long watchdog_events = 0;
 };
 
@@ -291,6 +294,22 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     IEngine& e;
     ~Unhook() { e.set_progress_hook(nullptr); }
   } unhook{e};
+  // Overlapped rounds: the slice may end with one replay still running, and the round
+  // below (status all-gather, plan, transfers) runs while it does — the reference's
+  // comm thread next to its GPU threads (pfsp_dist_multigpu_cuda.c:283,364-469). The
+  // status uses the last completed replay's counts (a pool with a replay in flight
+  // reports >= 1 node, so termination stays exact: it needs every pool empty with
+  // nothing in flight); a lower incumbent is applied at the next replay.
+  const bool overlap = o.overlap && share;
+  e.set_overlap(overlap);
+  struct NoOverlap {
+    IEngine& e;
+    bool on;
+    ~NoOverlap() {
+      if (on) e.set_overlap(false);
+    }
+  } no_overlap{e, overlap};
+  unsigned long long overlapped = 0;
 
   constexpr int kRec = 4;  // status record: pool size, incumbent, split pending, time up
   std::vector<int64_t> st(static_cast<size_t>(world) * kRec), sizes(world);
@@ -311,9 +330,11 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     const auto t1 = clock::now();
     t_run += secs(t0, t1);
     beat(1);
-    const int64_t size = static_cast<int64_t>(e.size());
-    const int mybest = e.best();
-    const bool pend = e.split_pending();
+    const bool flying = overlap && e.in_flight();
+    overlapped += flying;
+    const int64_t size = static_cast<int64_t>(flying ? e.size_known() : e.size());
+    const int mybest = flying ? e.best_known() : e.best();
+    const bool pend = flying ? e.split_pending_known() : e.split_pending();
     ctl.publish_size(size);
     wd_pool = size;
     wd_round = rounds;
@@ -358,7 +379,7 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
       total += sizes[r];
       starving |= sizes[r] < static_cast<int64_t>(o.needy_below);
     }
-    if (gbest < mybest) e.set_best(gbest);
+    if (gbest < mybest) e.offer_best(gbest);
     if (size == 0) t_idle += secs(t0, t2);
     if (total == 0) {  // every pool is empty and nothing is in flight: exact termination
       t_term += secs(t1, clock::now());
@@ -422,10 +443,11 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     }
   }
   beat(3);
+  if (overlap) e.set_overlap(false);  // waits for a replay still in flight (a time box / max_rounds stop)
 
   // ---- final reductions: two all-gathers (counters, times) ----
   const EngineStats es = e.stats();
-  constexpr int kIv = 15;
+  constexpr int kIv = 15;  // ShmControl::kMaxVals
   const int64_t iv[kIv] = {static_cast<int64_t>(es.tree), static_cast<int64_t>(es.sol), static_cast<int64_t>(sent),
                            static_cast<int64_t>(received), static_cast<int64_t>(tin), static_cast<int64_t>(tout),
                            static_cast<int64_t>(steals), static_cast<int64_t>(ssteals),
@@ -434,11 +456,12 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
                            static_cast<int64_t>(es.cpu_tree), static_cast<int64_t>(es.cpu_sol)};
   std::vector<int64_t> ia(static_cast<size_t>(world) * kIv);
   ctl.allgather(iv, kIv, ia.data(), [] {});
-  double dv[7] = {t_run, t_comm, t_idle, t_term, t_lb, es.t_memcpy, es.t_malloc};
-  int64_t dvi[7];
+  constexpr int kDv = 8;  // 7 timers + the overlapped-round count (exact as a double)
+  double dv[kDv] = {t_run, t_comm, t_idle, t_term, t_lb, es.t_memcpy, es.t_malloc, static_cast<double>(overlapped)};
+  int64_t dvi[kDv];
   std::memcpy(dvi, dv, sizeof(dv));
-  std::vector<int64_t> da(static_cast<size_t>(world) * 7);
-  ctl.allgather(dvi, 7, da.data(), [] {});
+  std::vector<int64_t> da(static_cast<size_t>(world) * kDv);
+  ctl.allgather(dvi, kDv, da.data(), [] {});
   out.rounds = rounds;
   out.best = 0x7fffffff;
   auto col = [&](int k) {
@@ -465,9 +488,10 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
   }
   auto dcol = [&](int k) {
     std::vector<double> v(world);
-    for (int r = 0; r < world; ++r) std::memcpy(&v[r], &da[r * 7 + k], sizeof(double));
+    for (int r = 0; r < world; ++r) std::memcpy(&v[r], &da[r * kDv + k], sizeof(double));
     return v;
   };
+  for (double x : dcol(7)) out.overlapped_rounds.push_back(static_cast<unsigned long long>(x));
   out.t_run = dcol(0);
   out.t_comm = dcol(1);
   out.t_idle = dcol(2);

@@ -39,6 +39,9 @@ struct EngineStats {
   unsigned long long tree = 0, sol = 0, parents = 0, iters = 0;
   int best = 0;
   unsigned long long launches = 0, syncs = 0, spilled = 0, refilled = 0, exports = 0, imports = 0;
+  // overlapped rounds: run() calls that returned with a replay in flight, and exports
+  // copied from under a running replay
+  unsigned long long left_inflight = 0, overlapped_exports = 0;
   size_t pinned_bytes = 0;  // pinned host spill blocks held
   double t_run = 0, t_memcpy = 0, t_malloc = 0;
   size_t device_nodes = 0, host_nodes = 0, capacity = 0;
@@ -85,6 +88,23 @@ class IEngine {
   virtual void record_event(uintptr_t ev) { (void)ev; }
   virtual void wait_event(uintptr_t ev) { (void)ev; }
   virtual void set_progress_hook(ProgressHook hook) { (void)hook; }
+  // Overlapped rounds (core/dist_rounds.hpp; ref pfsp_dist_multigpu_cuda.c:283,364-469,
+  // where the comm thread's collectives run while the GPU threads keep searching).
+  // With overlap on, run() may return with one replay still in flight when the pool
+  // holds several parent windows, so the round's all-gather, plan and transfers run
+  // while the GPU works. The *_known calls answer from the last completed replay
+  // without waiting (a pool with work in flight reports at least one node);
+  // offer_best applies a lower incumbent at the next replay; export_device may copy
+  // the pool bottom while the replay runs. Engines without in-flight work (CPU,
+  // multi/hybrid wrappers) keep the plain calls.
+  virtual void set_overlap(bool on) { (void)on; }
+  virtual bool in_flight() { return false; }
+  virtual size_t size_known() { return size(); }
+  virtual int best_known() { return best(); }
+  virtual bool split_pending_known() { return split_pending(); }
+  virtual void offer_best(int b) {
+    if (b < best()) set_best(b);
+  }
   // Sum over the pool of w[depth] (clamped to the last entry): with w[d] the share
   // of the search space below a node of depth d, 1 - pool_weight is the explored
   // fraction of the space (the B&B progress measure of tools/progress estimates).

@@ -280,6 +280,7 @@ class DeviceEngine final : public IEngine {
   // Stream-ordered (engine_api.hpp): no host wait unless spilled nodes must come back first.
   size_t export_device(void* dst, size_t max_n) override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    if (overlap_ && !inflight_.empty() && max_n > 0 && export_ahead(static_cast<Node*>(dst), max_n)) return max_n;
     settle();
     normalize();
     while (dev_stack() < max_n && !spill_.empty()) {
@@ -316,7 +317,37 @@ class DeviceEngine final : public IEngine {
   size_t size() override {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     sync_ctl();
+    commit_export();
     return dev_total() + spill_.size() + refill_n_;
+  }
+
+  // ---- overlapped rounds (engine_api.hpp) ----
+  void set_overlap(bool on) override {
+    TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+    overlap_ = on;
+    if (!on) {
+      sync_ctl();
+      commit_export();
+      apply_pending_best();
+    }
+  }
+  bool in_flight() override { return !inflight_.empty(); }
+  size_t size_known() override {
+    if (inflight_.empty()) return size();
+    const size_t known = dev_total() - export_pending_ + spill_.size() + refill_n_;
+    return std::max<size_t>(known, 1);
+  }
+  int best_known() override { return std::min(h_ctl_->best.v, pending_best_); }
+  bool split_pending_known() override {
+    if (inflight_.empty()) return split_pending();
+    return h_ctl_->split_world > 1 && !h_ctl_->slot[0].sdone;
+  }
+  void offer_best(int b) override {
+    if (!inflight_.empty()) {
+      pending_best_ = std::min(pending_best_, b);
+      return;
+    }
+    if (b < best()) set_best(b);
   }
 
   double pool_weight(const std::vector<double>& w) override {
@@ -354,11 +385,13 @@ class DeviceEngine final : public IEngine {
     auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
     long launches = 0;
     bool hook_stopped = false;
-    sync_ctl();
+    sync_ctl();  // a replay the previous (overlapped) run left in flight
     for (;;) {
       // ---- nothing in flight on the compute stream: the host shadow is the device state ----
       check_overflow();
       commit_spill_ahead();
+      commit_export();
+      apply_pending_best();
       poll_transfers();
       size_t total = dev_total();
       const size_t all = total + spill_.size() + refill_n_;
@@ -371,8 +404,12 @@ class DeviceEngine final : public IEngine {
       }
       if (all < stop_below) break;
       if (max_launches >= 0 && launches >= max_launches) break;
-      if (max_seconds > 0 && elapsed() >= max_seconds) break;
-      if (hook_stopped) break;  // the hook asked to stop during the last pipelined stretch
+      if ((max_seconds > 0 && elapsed() >= max_seconds) || hook_stopped) {
+        // overlapped rounds: the slice is over, but a pool of several windows keeps the
+        // GPU busy with one more replay while the caller's round runs
+        if (leave_one(total)) ++launches;
+        break;
+      }
       if (hook_) {
         int b = h_ctl_->best.v;
         const bool stop = hook_(all, b);
@@ -380,7 +417,10 @@ class DeviceEngine final : public IEngine {
           h_ctl_->best.v = b;
           upload_ctl();
         }
-        if (stop) break;
+        if (stop) {
+          if (leave_one(total)) ++launches;
+          break;
+        }
       }
       // refill ahead of need from the pinned spill, one pinned block at a time, while
       // the device still holds work for the next replays to overlap the copy with
@@ -429,10 +469,17 @@ class DeviceEngine final : public IEngine {
       // sync + launch gap between replays. ----
       size_t known = total;
       size_t inflight_growth = static_cast<size_t>((kf ? kf : ks_[gi]) + 1) * buf_nodes_;
-      bool hook_stop = false;
+      bool hook_stop = false, leaving = false;
       while (!inflight_.empty()) {
         const bool budget_ok = !hook_stop && (max_launches < 0 || launches < max_launches) &&
                                (max_seconds <= 0 || elapsed() < max_seconds);
+        // overlapped rounds: the slice ends with the last pipelined replay still running
+        if (overlap_ && !budget_ok && inflight_.size() == 1 && (max_launches < 0 || launches < max_launches) &&
+            leave_ok(known)) {
+          leaving = true;
+          ++stats_.left_inflight;
+          break;
+        }
         if (inflight_.size() == 1 && budget_ok && known >= spec_min_) {
           const int g2 = pick_graph(known, inflight_growth);
           if (g2 >= 0) {
@@ -454,11 +501,8 @@ class DeviceEngine final : public IEngine {
           if (b < pending_best_) pending_best_ = b;
         }
       }
-      if (pending_best_ < h_ctl_->best.v) {
-        h_ctl_->best.v = pending_best_;
-        upload_ctl();
-      }
-      pending_best_ = 0x7fffffff;
+      if (leaving) break;  // pending_best_ is applied after the replay (apply_pending_best)
+      apply_pending_best();
       hook_stopped = hook_stop;
     }
     stats_.t_run += elapsed();
@@ -646,6 +690,59 @@ class DeviceEngine final : public IEngine {
   }
 
  private:
+  // Overlapped rounds: may a replay run on while the caller does its round? The pool
+  // must hold enough that the replay cannot run dry (and its donors can export from
+  // under it), and no rank split may be pending (the split replays every level).
+  bool leave_ok(size_t total) const {
+    return overlap_ && total >= 2 * cfg_.max_parents && !(h_ctl_->split_world > 1 && !h_ctl_->slot[0].sdone);
+  }
+  // Nothing in flight: launch one replay and leave it running (returns true if launched).
+  bool leave_one(size_t total) {
+    if (!leave_ok(total) || !inflight_.empty()) return false;
+    const int gi = pick_graph(total, 0);
+    if (gi < 0) return false;
+    launch_graph(gi);
+    start_spill_ahead();
+    ++stats_.left_inflight;
+    return true;
+  }
+  // Export from under running replays: the replays in flight pop at most their
+  // iterations x window parents from the top, so the oldest nodes above that (plus one
+  // window of margin) are read by no replay; they were written by completed ones. The
+  // copy runs on the transfer stream now; the nodes leave the host shadow's stack when
+  // the replays have completed (commit_export).
+  bool export_ahead(Node* dst, size_t n) {
+    if (ahead_n_ || refill_n_ || !resv_.empty()) return false;
+    size_t k = 0;
+    for (int x : inflight_k_) k += static_cast<size_t>(x);
+    const size_t safe = (k + 1) * cfg_.max_parents;
+    const size_t stack = dev_stack() - export_pending_;
+    if (stack < n + safe) return false;
+    const size_t start = (h_ctl_->bot + export_pending_) & (cap_ - 1);
+    const size_t first = std::min(n, cap_ - start);
+    TTS_HIP_CHECK(hipMemcpyAsync(dst, d_ring_ + start, first * sizeof(Node), hipMemcpyDeviceToDevice, xfer_));
+    if (first < n)
+      TTS_HIP_CHECK(hipMemcpyAsync(dst + first, d_ring_, (n - first) * sizeof(Node), hipMemcpyDeviceToDevice, xfer_));
+    export_pending_ += n;
+    ++stats_.exports;
+    ++stats_.overlapped_exports;
+    return true;
+  }
+  void commit_export() {
+    if (!export_pending_ || !inflight_.empty()) return;
+    h_ctl_->bot = (h_ctl_->bot + export_pending_) & (cap_ - 1);
+    h_ctl_->slot[0].stack -= export_pending_;
+    export_pending_ = 0;
+    upload_ctl();
+  }
+  void apply_pending_best() {
+    if (pending_best_ < h_ctl_->best.v && inflight_.empty()) {
+      h_ctl_->best.v = pending_best_;
+      upload_ctl();
+    }
+    if (inflight_.empty()) pending_best_ = 0x7fffffff;
+  }
+
   void check_overflow() {
     if (h_ctl_->overflow == 2)
       throw std::runtime_error("pool outgrew the parent window before the armed rank split (set_split)");
@@ -661,6 +758,8 @@ class DeviceEngine final : public IEngine {
   // (every host edit is uploaded from it).
   void sync_ctl() {
     while (!inflight_.empty()) wait_oldest();
+    commit_export();
+    apply_pending_best();
   }
   // The finalize kernel publishes the mirror's sequence word last (release, system
   // scope): spinning on it returns as soon as the block is in host memory, without
@@ -788,6 +887,8 @@ class DeviceEngine final : public IEngine {
   void settle() {
     flush_load();
     sync_ctl();
+    commit_export();
+    apply_pending_best();
     commit_spill_ahead();
     if (refill_n_) finish_refill();
     poll_transfers();
@@ -1052,6 +1153,8 @@ class DeviceEngine final : public IEngine {
   hipEvent_t refill_ev_ = nullptr;
   ProgressHook hook_;
   int pending_best_ = 0x7fffffff;  // incumbent handed in by the hook while graphs were in flight
+  bool overlap_ = false;           // overlapped rounds (set_overlap)
+  size_t export_pending_ = 0;      // exported from under running replays, not yet off the shadow
   int next_mirror_ = 0;
   std::deque<int> inflight_, inflight_k_;
   std::deque<dev::u64> inflight_seq_;

@@ -30,6 +30,16 @@ for step in "$@"; do
       cat "$out/bench_n1.json" ;;
     ktrace:*)
       bash scripts/gpu_run.sh "${out#gpurun_out/}" "$step" || exit 1 ;;
+    rccl)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_rccl.py -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$out/rccl_tests.log" 2>&1 || { tail -30 "$out/rccl_tests.log"; exit 1; }
+      tail -3 "$out/rccl_tests.log" ;;
+    shared2:*)  # shared2:<extras>: 2 ranks on one GPU (gloo), headline + extras, overlap on
+      ex="${step#shared2:}"
+      timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --comm gloo --device 0 --extras "$ex" \
+        > "$out/bench_n2_shared.json" 2> "$out/bench_n2_shared.err" || { tail -20 "$out/bench_n2_shared.err"; exit 1; }
+      cat "$out/bench_n2_shared.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
