@@ -215,6 +215,7 @@ inline DistOptions dist_options_from(const py::dict& o) {
   get("time_limit", opt.time_limit);
   get("live_best", opt.live_best);
   get("overlap", opt.overlap);
+  get("trace_incumbent", opt.trace_incumbent);
   get("checkpoint_every", opt.checkpoint_every);
   get("watchdog_s", opt.watchdog_s);
   get("watchdog_abort", opt.watchdog_abort);
@@ -292,6 +293,9 @@ inline py::dict outcome_dict(const DistOutcome& out) {
                      // early_rounds dropped cpu_tree cpu_sol (CPU-worker share of a hybrid rank)
   d["times"] = fv;   // t_run t_comm t_idle t_termination t_load_bal t_memcpy t_malloc
   d["overlapped_rounds"] = out.overlapped_rounds;  // rounds with a replay in flight, per rank
+  py::list ev;  // this rank's incumbent timeline (trace_incumbent)
+  for (const auto& x : out.incumbent_events) ev.append(py::make_tuple(x[0], x[1], x[2], x[3]));
+  d["incumbent_events"] = ev;
   return d;
 }
 

@@ -120,6 +120,12 @@ PYBIND11_MODULE(_tts_hip, m) {
   bind_runner(
       m, []() -> std::unique_ptr<DeviceStaging> { return std::make_unique<HipStaging>(); }, &device_cpus);
   if (!std::getenv("TTS_NO_ROCTX")) install_roctx_hooks();
+  // release every engine / RCCL communicator while the HIP runtime is alive (atexit
+  // handlers run before interpreter teardown; csrc/hip/device_resource.hpp)
+  m.def("release_all", &DeviceResource::release_all,
+        "Free the device resources of every live engine and RCCL transport (also run at exit).");
+  m.def("live_resources", &DeviceResource::live_count);
+  py::module_::import("atexit").attr("register")(py::cpp_function([]() { DeviceResource::release_all(); }));
   m.def("device_pci_bus_id", &device_pci_bus_id);
   m.def("device_cpus", &device_cpus, "CPUs of the NUMA node closest to the GPU (empty if unknown).");
 

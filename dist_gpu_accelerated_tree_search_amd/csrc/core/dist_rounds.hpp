@@ -23,6 +23,7 @@
 #pragma once
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -196,6 +197,7 @@ struct DistOptions {
                                                   // on any rank (0: never; throughput time boxes)
   bool live_best = true;                          // exchange the incumbent after every replay (board)
   bool overlap = true;                            // rounds overlap a running replay (IEngine::set_overlap)
+  bool trace_incumbent = false;                   // record this rank's incumbent timeline (diagnostics)
   long checkpoint_every = 0;                      // RoundHook every k rounds (0: never)
   double watchdog_s = 0;                          // report a phase longer than this
   bool watchdog_abort = false;
@@ -215,6 +217,11 @@ struct DistOutcome {
   std::vector<double> t_run, t_comm, t_idle, t_termination, t_load_bal, t_memcpy, t_malloc;
   // rounds this rank spent with a replay in flight (the GPU searching during the round)
   std::vector<unsigned long long> overlapped_rounds;
+  // trace_incumbent (this rank only): after every replay where the incumbent changed,
+  // {seconds since the rounds began, explored tree so far (engine), own incumbent
+  // before the exchange, incumbent after it}; the source of a change is the engine's
+  // own leaves when the own value dropped, a peer when only the exchanged one did
+  std::vector<std::array<double, 4>> incumbent_events;
   unsigned long long watchdog_events = 0;
 };
 
@@ -285,9 +292,17 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
   // the slice on a peer's request ----
   ctl.begin_solve();
   const bool live_best = o.live_best && world > 1;
+  const auto t_hook0 = clock::now();
+  int last_seen = 0x7fffffff;
   e.set_progress_hook([&](size_t pool, int& best) {
     ctl.publish_size(static_cast<int64_t>(pool));
+    const int own = best;
     if (live_best) best = std::min(best, ctl.exchange_best(best));
+    if (o.trace_incumbent && best < last_seen) {
+      out.incumbent_events.push_back({secs(t_hook0, clock::now()), static_cast<double>(e.tree_known()),
+                                      static_cast<double>(own), static_cast<double>(best)});
+      last_seen = best;
+    }
     return board && ctl.round_requested();
   });
   struct Unhook {

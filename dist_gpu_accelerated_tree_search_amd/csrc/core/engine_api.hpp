@@ -105,6 +105,9 @@ class IEngine {
   virtual void offer_best(int b) {
     if (b < best()) set_best(b);
   }
+  // Explored tree as of the last completed replay, without waiting (diagnostics from
+  // the progress hook; 0 where unknown)
+  virtual unsigned long long tree_known() { return 0; }
   // Sum over the pool of w[depth] (clamped to the last entry): with w[d] the share
   // of the search space below a node of depth d, 1 - pool_weight is the explored
   // fraction of the space (the B&B progress measure of tools/progress estimates).

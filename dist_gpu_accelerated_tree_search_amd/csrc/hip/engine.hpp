@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../core/engine_api.hpp"
+#include "device_resource.hpp"
 #include "host_spill.hpp"
 #include "pool_device.hpp"
 
@@ -42,7 +43,7 @@ namespace tts {
 //   static void finalize(const dev::PoolArgs<Node>&, hipStream_t);
 //   static int blocks_per_cu();
 template <class Traits>
-class DeviceEngine final : public IEngine {
+class DeviceEngine final : public IEngine, public DeviceResource {
  public:
   using Node = typename Traits::Node;
   using Args = typename Traits::Args;
@@ -163,12 +164,18 @@ class DeviceEngine final : public IEngine {
     stats_.t_malloc = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
-  ~DeviceEngine() override {
+  ~DeviceEngine() override { release(); }
+
+  // Every device / pinned resource of the engine (DeviceResource: also from the
+  // module's atexit hook, before runtime teardown). Idempotent.
+  void release() override {
+    if (released_) return;
+    released_ = true;
     (void)hipSetDevice(cfg_.device);
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (xfer_) (void)hipStreamSynchronize(xfer_);
     trace_clear();
-    spill_.clear();
+    spill_.free_all();
     for (auto& gp : graphs_)
       for (auto& gs : gp)
         for (auto g : gs) (void)hipGraphExecDestroy(g);
@@ -194,6 +201,13 @@ class DeviceEngine final : public IEngine {
     (void)hipEventDestroy(ev_xfer_);
     if (xfer_) (void)hipStreamDestroy(xfer_);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
+    graphs_[0][0].clear();
+    graphs_[0][1].clear();
+    graphs_[1][0].clear();
+    graphs_[1][1].clear();
+    first_graphs_.clear();
+    owned_.clear();
+    xfer_ = own_stream_ = stream_ = nullptr;
   }
 
   size_t node_bytes() const override { return sizeof(Node); }
@@ -338,6 +352,11 @@ class DeviceEngine final : public IEngine {
     return std::max<size_t>(known, 1);
   }
   int best_known() override { return std::min(h_ctl_->best.v, pending_best_); }
+  unsigned long long tree_known() override {
+    unsigned long long t = h_ctl_->tree + h_ctl_->pend_children + h_ctl_->pend_internal;
+    for (const auto& x : h_ctl_->xacc) t += x.tree;
+    return t;
+  }
   bool split_pending_known() override {
     if (inflight_.empty()) return split_pending();
     return h_ctl_->split_world > 1 && !h_ctl_->slot[0].sdone;
@@ -380,6 +399,7 @@ class DeviceEngine final : public IEngine {
   }
 
   long run(long max_launches, double max_seconds, size_t stop_below) override {
+    if (released_) throw std::runtime_error("engine closed");
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     const auto t0 = std::chrono::steady_clock::now();
     auto elapsed = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
@@ -512,6 +532,7 @@ class DeviceEngine final : public IEngine {
   // Fused start of a solve: fresh counters and incumbent, `n` nodes loaded at the
   // ring base, one asynchronous control upload (no stream synchronisation).
   void begin(const void* nodes, size_t n, int best) override {
+    if (released_) throw std::runtime_error("engine closed");
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     settle();
     normalize();
@@ -1152,6 +1173,7 @@ class DeviceEngine final : public IEngine {
   std::deque<std::pair<hipEvent_t, size_t>> ahead_;
   hipEvent_t refill_ev_ = nullptr;
   ProgressHook hook_;
+  bool released_ = false;          // release(): nothing left to free
   int pending_best_ = 0x7fffffff;  // incumbent handed in by the hook while graphs were in flight
   bool overlap_ = false;           // overlapped rounds (set_overlap)
   size_t export_pending_ = 0;      // exported from under running replays, not yet off the shadow

@@ -35,9 +35,15 @@ class PinnedSpill {
   };
 
   explicit PinnedSpill(size_t block_nodes) : block_nodes_(std::max<size_t>(1, block_nodes)) {}
-  ~PinnedSpill() {
+  ~PinnedSpill() { free_all(); }
+  // Every pinned block back to the runtime now (the engine's release(), before runtime
+  // teardown); the spill is empty and unusable for copies in flight afterwards.
+  void free_all() {
     for (auto& b : blocks_) release(b);
     for (auto& b : free_) release(b);
+    blocks_.clear();
+    free_.clear();
+    n_ = 0;
   }
   PinnedSpill(const PinnedSpill&) = delete;
   PinnedSpill& operator=(const PinnedSpill&) = delete;

@@ -25,6 +25,7 @@
 #include "../core/dist_rounds.hpp"
 #include "../core/engine_api.hpp"
 #include "device_common.hpp"
+#include "device_resource.hpp"
 
 #define TTS_NCCL_CHECK(expr)                                                                               \
   do {                                                                                                     \
@@ -36,7 +37,7 @@
 
 namespace tts {
 
-class RcclTransport {
+class RcclTransport final : public DeviceResource {
  public:
   static std::vector<uint8_t> new_id() {
     ncclUniqueId id;
@@ -53,14 +54,19 @@ class RcclTransport {
     TTS_HIP_CHECK(hipSetDevice(device_));
     TTS_NCCL_CHECK(ncclCommInitRank(&comm_, world, uid, rank));
   }
-  ~RcclTransport() {
+  ~RcclTransport() override { release(); }
+  void release() override {
+    if (released_) return;
+    released_ = true;
     (void)hipSetDevice(device_);
     for (int b = 0; b < 2; ++b)
       if (buf_[b]) {
         (void)hipDeviceSynchronize();
         (void)hipFree(buf_[b]);
+        buf_[b] = nullptr;
       }
     if (comm_) (void)ncclCommDestroy(comm_);
+    comm_ = nullptr;
   }
   RcclTransport(const RcclTransport&) = delete;
   RcclTransport& operator=(const RcclTransport&) = delete;
@@ -75,6 +81,7 @@ class RcclTransport {
   // The plan's transfers that concern this rank (every rank calls this with the same
   // plan, in the same round); returns (nodes sent, nodes received).
   std::pair<size_t, size_t> execute(const Plan& plan, IEngine& e) {
+    if (released_) throw std::runtime_error("RCCL transport closed");
     size_t nout = 0, nin = 0;
     const std::vector<P2PCall> calls = p2p_calls(plan, rank_, &nout, &nin);
     if (calls.empty()) return {0, 0};
@@ -212,6 +219,7 @@ class RcclTransport {
   }
 
   ncclComm_t comm_ = nullptr;
+  bool released_ = false;
   int rank_, world_, device_;
   void* buf_[2] = {nullptr, nullptr};
   size_t cap_[2] = {0, 0};

@@ -85,6 +85,12 @@ class DistConfig:
     # exchange the incumbent through the node-wide board after every graph replay
     # (ref checkBest around every batch); False: only at round boundaries
     live_best: bool = True
+    # overlapped rounds: a rank's slice may end with one graph replay still running,
+    # and the round (all-gather, plan, transfers) runs while it does (ref: the comm
+    # thread next to the GPU threads, pfsp_dist_multigpu_cuda.c:283,364-469)
+    overlap: bool = True
+    # record every rank's incumbent timeline (extra["incumbent_events"], diagnostics)
+    trace_incumbent: bool = False
     # CPU worker next to each rank's GPU (ref -C 1 in pfsp_dist_multigpu_cuda.c:161-162,
     # 471-575): threads of the rank's CPU engine (0: none) and its batch (ref -T; a CPU
     # thief takes at most 4*T nodes). parallel/workers.py wraps the engines into one
@@ -205,7 +211,8 @@ def _native_options(cfg: DistConfig, engine, comm: Comm, window: int | None):
     opts = dict(needy_below=needy, donor_min=donor, steal_cap=cfg.steal_cap, slice_min=cfg.slice_min_s,
                 slice_max=cfg.slice_max_s, intra=bool(cfg.ws and share), inter=bool(cfg.L and share),
                 local_world=comm.topo.local_world, early_rounds=cfg.early_rounds, max_rounds=cfg.max_rounds,
-                time_limit=float(cfg.time_limit_s), live_best=bool(cfg.live_best),
+                time_limit=float(cfg.time_limit_s), live_best=bool(cfg.live_best), overlap=bool(cfg.overlap),
+                trace_incumbent=bool(cfg.trace_incumbent),
                 checkpoint_every=cfg.checkpoint_every if cfg.checkpoint_dir else 0,
                 watchdog_s=float(cfg.watchdog_s or float(env.get("TTS_WATCHDOG_S", "0") or 0)),
                 watchdog_abort=bool(cfg.watchdog_abort or env.get("TTS_WATCHDOG_ABORT", "0") not in ("", "0")),
@@ -262,7 +269,9 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, t_start: float, t_init: 
                               "received_nodes": cnt[:, 3].tolist(), "world": world,
                               "complete": bool(out["complete"]), "dropped_transfers": int(cnt[:, 10].sum()),
                               "watchdog_events": int(out["watchdog_events"]),
-                              "early_rounds": cnt[:, 9].tolist(), "needy_below": needy, "donor_min": donor})
+                              "early_rounds": cnt[:, 9].tolist(), "needy_below": needy, "donor_min": donor,
+                              "overlapped_rounds": list(out.get("overlapped_rounds", [])),
+                              "incumbent_events": list(out.get("incumbent_events", []))})
 
 
 class RankTable(list):
@@ -358,4 +367,6 @@ class DistSolver:
                                   "complete": bool(complete), "dropped_transfers": int(cnt[:, 10].sum()),
                                   "watchdog_events": int(out["watchdog_events"]),
                                   "early_rounds": cnt[:, 9].tolist(), "needy_below": self.needy,
-                                  "donor_min": self.donor})
+                                  "donor_min": self.donor,
+                                  "overlapped_rounds": list(out.get("overlapped_rounds", [])),
+                                  "incumbent_events": list(out.get("incumbent_events", []))})
