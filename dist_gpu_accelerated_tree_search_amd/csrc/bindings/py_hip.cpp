@@ -273,7 +273,7 @@ PYBIND11_MODULE(_tts_hip, m) {
       "pfsp_front_probe",
       [](int jobs, int machines, std::vector<int> p, int lb, U8 nodes, int best, int device, size_t max_parents,
          int fuse_max, int deep_levels, int deep_per3, int deep_per4, int local_steps, unsigned cap, int split_rank,
-         int split_world, size_t split_min) {
+         int split_world, size_t split_min, int wide_levels) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p));
         EngineConfig c;
         c.device = device;
@@ -284,6 +284,7 @@ PYBIND11_MODULE(_tts_hip, m) {
         c.deep_per3 = deep_per3;
         c.deep_per4 = deep_per4;
         c.local_steps = local_steps;
+        c.wide_levels = wide_levels;
         FrontProbeResult r;
         {
           py::gil_scoped_release nogil;
@@ -311,12 +312,13 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 16, py::arg("fuse_max") = 1 << 30,
       py::arg("deep_levels") = 4, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("local_steps") = 4,
       py::arg("cap") = 1u << 22, py::arg("split_rank") = 0, py::arg("split_world") = 1, py::arg("split_min") = 0,
+      py::arg("wide_levels") = 2,
       "A complete front-kernel engine solve from these (front-layout) nodes with probe records on: every child "
       "bound of every iteration shape checked against the host oracle (counts of records and mismatches).");
   m.def(
       "pfsp_front_time",
       [](int jobs, int machines, std::vector<int> p, int lb, U8 nodes, int best, int device, size_t max_parents,
-         int fuse_max, int deep_levels, int deep_per3, int deep_per4, int reps) {
+         int fuse_max, int deep_levels, int deep_per3, int deep_per4, int reps, int wide_levels) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p));
         EngineConfig c;
         c.device = device;
@@ -325,6 +327,7 @@ PYBIND11_MODULE(_tts_hip, m) {
         c.deep_levels = deep_levels;
         c.deep_per3 = deep_per3;
         c.deep_per4 = deep_per4;
+        c.wide_levels = wide_levels;
         std::vector<double> t;
         {
           py::gil_scoped_release nogil;
@@ -344,6 +347,7 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("nodes"), py::arg("best"),
       py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 19, py::arg("fuse_max") = 1 << 30,
       py::arg("deep_levels") = 4, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("reps") = 20,
+      py::arg("wide_levels") = 2,
       "Time one front-kernel iteration over this window: min / median ms, and the per-workgroup phase stamps.");
   m.def(
       "queens_labels",

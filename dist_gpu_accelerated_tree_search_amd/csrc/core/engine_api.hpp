@@ -31,6 +31,7 @@ struct EngineConfig {
   int deep_levels = 4;                   // fused iterations: at most this many tree levels (kernels that have them)
   int deep_per3 = 8;                     // ... 3 levels when a workgroup takes at most this many parents
   int deep_per4 = 2;                     // ... 4 levels when a workgroup takes at most this many parents
+  int wide_levels = 2;                   // wide windows (<= one parent per thread): levels per iteration (< 2: off)
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };

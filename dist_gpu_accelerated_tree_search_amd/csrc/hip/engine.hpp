@@ -132,6 +132,8 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (const char* f = std::getenv("TTS_DEEP_LEVELS")) pa.deep_levels = std::max(2, std::atoi(f));
     if (const char* f = std::getenv("TTS_DEEP_P3")) pa.deep_per[0] = std::max(0, std::atoi(f));
     if (const char* f = std::getenv("TTS_DEEP_P4")) pa.deep_per[1] = std::max(0, std::atoi(f));
+    pa.wide_levels = cfg_.wide_levels;
+    if (const char* f = std::getenv("TTS_WIDE_LEVELS")) pa.wide_levels = std::atoi(f);
     grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, resident)));
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known

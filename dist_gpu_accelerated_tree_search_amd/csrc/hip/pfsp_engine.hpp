@@ -592,6 +592,8 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   pa.deep_levels = cfg.deep_levels;
   pa.deep_per[0] = cfg.deep_per3;
   pa.deep_per[1] = cfg.deep_per4;
+  pa.wide_levels = cfg.wide_levels;
+  if (const char* f = std::getenv("TTS_WIDE_LEVELS")) pa.wide_levels = std::atoi(f);
   int bpc = 0, cus = 0;
   bpc = PfspFrontTraits<M>::blocks_per_cu();
   if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(g));  // as DeviceEngine

@@ -50,6 +50,7 @@ struct FrontGeom {
   // one workgroup per CU wait for another to finish)
   static constexpr int CAP = 96;
   static constexpr int LMAX = 4;
+  static constexpr int WLMAX = 3;  // levels of a wide multi-level chunk (one thread per window parent first)
   // a level of at most CPMAX children is expanded child-parallel (one thread per child),
   // a wider one one thread per node (each runs its children in turn)
   static constexpr int CPMAX = 3 * 256;
@@ -362,30 +363,13 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
 // scan) and handed to store(index, child words, child remain). Wider levels take this
 // path: fewer instructions per child than front_expand_cp (no parent search, one node
 // load per parent), and the serial loop is short once most lanes hold a node.
+// (the node and its packed remain in registers; w = 0 for a thread without a node)
 template <int M, class Store>
-__device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm,
-                                      const uint4 (*src)[FrontGeom<M>::VPN], const uint32_t (*rem)[FrontGeom<M>::HW],
-                                      int n, int best, int& nleaf, Store store) {
+__device__ inline int front_expand_tp_regs(const PfspFrontArgs<M>& a, FrontSmem<M>& sm,
+                                           const uint32_t (&w)[FrontGeom<M>::NW], const uint32_t (&rp)[FrontGeom<M>::HW],
+                                           int best, int& nleaf, Store store, int kind = kDbgTp) {
   using G = FrontGeom<M>;
   constexpr int HW = G::HW;
-  const int tid = threadIdx.x;
-  uint32_t w[G::NW], rp[HW];
-#pragma unroll
-  for (int i = 0; i < G::NW; ++i) w[i] = 0;
-#pragma unroll
-  for (int h = 0; h < HW; ++h) rp[h] = 0;
-  if (tid < n) {
-#pragma unroll
-    for (int q = 0; q < G::VPN; ++q) {
-      const uint4 x = src[tid][q];
-      w[4 * q] = x.x;
-      w[4 * q + 1] = x.y;
-      w[4 * q + 2] = x.z;
-      w[4 * q + 3] = x.w;
-    }
-#pragma unroll
-    for (int h = 0; h < HW; ++h) rp[h] = rem[tid][h];
-  }
   uint32_t surv = 0;
   int nsurv = 0;
   const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
@@ -408,7 +392,7 @@ __device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
         lb = max(lb, sv + r[m]);
         tt = sv + pr[m];
       }
-      if (a.dbg_rec) front_dbg<M>(a, kDbgTp, w, rp, j, lb);
+      if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
       if (leaf) {
         ++nleaf;
         if (lb < best) atomicMin(&a.pool.ctl->best.v, lb);
@@ -433,6 +417,46 @@ __device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
   return tot;
 }
 
+template <int M, class Store>
+__device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm,
+                                      const uint4 (*src)[FrontGeom<M>::VPN], const uint32_t (*rem)[FrontGeom<M>::HW],
+                                      int n, int best, int& nleaf, Store store) {
+  using G = FrontGeom<M>;
+  constexpr int HW = G::HW;
+  const int tid = threadIdx.x;
+  uint32_t w[G::NW], rp[HW];
+#pragma unroll
+  for (int i = 0; i < G::NW; ++i) w[i] = 0;
+#pragma unroll
+  for (int h = 0; h < HW; ++h) rp[h] = 0;
+  if (tid < n) {
+#pragma unroll
+    for (int q = 0; q < G::VPN; ++q) {
+      const uint4 x = src[tid][q];
+      w[4 * q] = x.x;
+      w[4 * q + 1] = x.y;
+      w[4 * q + 2] = x.z;
+      w[4 * q + 3] = x.w;
+    }
+#pragma unroll
+    for (int h = 0; h < HW; ++h) rp[h] = rem[tid][h];
+  }
+  return front_expand_tp_regs<M>(a, sm, w, rp, best, nleaf, store);
+}
+
+// The packed remain of the node in w: the sum of its unscheduled jobs' p rows.
+template <int M>
+__device__ inline void front_remain(const FrontSmem<M>& sm, const uint32_t (&w)[FrontGeom<M>::NW],
+                                    uint32_t (&r2)[FrontGeom<M>::HW]) {
+#pragma unroll
+  for (int h = 0; h < FrontGeom<M>::HW; ++h) r2[h] = 0;
+  for (uint32_t x = w[1]; x; x &= x - 1) {
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[__builtin_ctz(x)]);
+#pragma unroll
+    for (int h = 0; h < FrontGeom<M>::HW; ++h) r2[h] += row[h];
+  }
+}
+
 // Multi-level chunk (fused iterations): the chunk's v.bp parents go to LDS with their
 // remains, then up to v.levels tree levels are expanded in place — each level's
 // survivors become the next level's nodes in the other LDS buffer (at most CAP of them;
@@ -449,39 +473,65 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
   using Node = PfspFrontNode<M>;
   static_assert(G::BPF_CP * (G::NJ - 1) + (G::LMAX - 1) * G::CAP * (G::NJ - 1) <= G::SLOT,
                 "chunk output must fit its slot region");
+  static_assert(kBlock * (G::NJ - 1) + (G::WLMAX - 1) * G::CAP * (G::NJ - 1) <= G::SLOT,
+                "wide chunk output must fit its slot region");
   static_assert(G::CAP <= kBlock && G::BPF_CP <= G::CAP, "one thread per staged node");
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  const int L = min(v.levels, G::LMAX);
+  // wide chunks (more parents than a staged level holds): the first level runs one
+  // thread per window parent straight from the pool, its survivors go to LDS
+  const bool wide = v.bp > G::BPF_CP;
+  const int L = min(v.levels, wide ? G::WLMAX : G::LMAX);
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     const u64 g0 = static_cast<u64>(ch) * v.bp;
     const int n0 = static_cast<int>(min(static_cast<u64>(v.bp), v.B - g0));
-    if (tid < n0) {
-      // the parent's remain: one pass over its unscheduled rows (packed u16 pairs; sums
-      // < 65536, pfsp_front_ok), by the thread that stages it
-      uint32_t w[G::NW];
-      front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
-      front_store<M>(&sm.lvl[0][tid][0], w);
-      uint32_t r2[G::HW];
-#pragma unroll
-      for (int h = 0; h < G::HW; ++h) r2[h] = 0;
-      for (uint32_t x = w[1]; x; x &= x - 1) {
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[__builtin_ctz(x)]);
-#pragma unroll
-        for (int h = 0; h < G::HW; ++h) r2[h] += row[h];
-      }
-#pragma unroll
-      for (int h = 0; h < G::HW; ++h) sm.rlv[0][tid][h] = r2[h];
-    }
-    __syncthreads();
-    const bool first = ch == static_cast<int>(blockIdx.x);
-    if (first) front_stamp(a, 3);
-    int nleaf = 0, inner = 0, o = 0, n = n0, cur = 0;
+    int nleaf = 0, inner = 0, o = 0, n = n0, cur = 0, lev0 = 0;
     uint4* const out = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
-    for (int lev = 0; lev < L && n > 0; ++lev) {
+    const bool first = ch == static_cast<int>(blockIdx.x);
+    if (wide) {
+      uint32_t w[G::NW], r2[G::HW];
+#pragma unroll
+      for (int i = 0; i < G::NW; ++i) w[i] = 0;
+      if (tid < n0) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
+      front_remain<M>(sm, w, r2);
+      const bool last = L == 1;
+      const int nn = front_expand_tp_regs<M>(
+          a, sm, w, r2, best, nleaf,
+          [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {
+            if (!last && i < G::CAP) {
+              front_store<M>(&sm.lvl[1][i][0], c);
+#pragma unroll
+              for (int h = 0; h < G::HW; ++h) sm.rlv[1][i][h] = r[h];
+            } else {
+              front_store<M>(out + (last ? i : i - G::CAP) * G::VPN, c);
+            }
+          },
+          kDbgOne);
+      __syncthreads();
+      o = last ? nn : max(0, nn - G::CAP);
+      n = last ? 0 : min(nn, G::CAP);
+      inner = n;
+      cur = 1;
+      lev0 = 1;
+      if (first) front_stamp(a, 4);
+    } else {
+      if (tid < n0) {
+        // the parent's remain: one pass over its unscheduled rows (packed u16 pairs; sums
+        // < 65536, pfsp_front_ok), by the thread that stages it
+        uint32_t w[G::NW], r2[G::HW];
+        front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
+        front_store<M>(&sm.lvl[0][tid][0], w);
+        front_remain<M>(sm, w, r2);
+#pragma unroll
+        for (int h = 0; h < G::HW; ++h) sm.rlv[0][tid][h] = r2[h];
+      }
+      __syncthreads();
+    }
+    if (first) front_stamp(a, 3);
+    for (int lev = lev0; lev < L && n > 0; ++lev) {
       const bool last = lev == L - 1;
       const int nx = cur ^ 1;
       auto store = [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {

@@ -86,6 +86,9 @@ struct PoolArgs {
   // (capped by deep_levels); 2 levels otherwise
   int deep_levels;
   int deep_per[2];
+  // wide multi-level iterations: a window of more than a narrow chunk's parents per
+  // workgroup but at most one per thread is expanded this many levels deep (< 2: off)
+  int wide_levels;
 };
 
 // Per-chunk leaf word: leaves in the low 16 bits; the high 16 bits count the
@@ -259,6 +262,13 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     const int lmax = min(LMAX, pa.deep_levels);
     if (!armed && lmax >= 3 && per <= static_cast<u64>(pa.deep_per[0])) v.levels = 3;
     if (!armed && lmax >= 4 && per <= static_cast<u64>(pa.deep_per[1])) v.levels = 4;
+  } else if (LMAX > 2 && !v.local && !armed && pa.wide_levels >= 2 && v.B <= static_cast<u64>(pa.fuse_max) &&
+             (v.B + gridDim.x - 1) / gridDim.x <= static_cast<u64>(BP)) {
+    // wide multi-level: every workgroup takes one chunk of up to one parent per thread
+    // (the kernel's first level runs from the pool, the next ones from LDS)
+    v.fused = true;
+    bp = static_cast<int>(max((v.B + gridDim.x - 1) / gridDim.x, 1ull));
+    v.levels = min(pa.wide_levels, LMAX);
   }
   if (v.local) {
     // spread a window smaller than the grid over every workgroup

@@ -22,8 +22,12 @@ m = PfspModel(inst, lb)
 H = ops.require_gpu(0)
 best = m.best_known
 depths = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else list(range(2, 20))
-shapes = [("one", dict(fuse_max=0)), ("L2", dict(deep_levels=2)), ("L3", dict(deep_levels=3, deep_per3=1 << 20)),
-          ("L4", dict(deep_levels=4, deep_per3=1 << 20, deep_per4=1 << 20))]
+shapes = [("one", dict(fuse_max=0)), ("L2", dict(deep_levels=2, wide_levels=1)),
+          ("L3", dict(deep_levels=3, deep_per3=1 << 20, wide_levels=1)),
+          ("L4", dict(deep_levels=4, deep_per3=1 << 20, deep_per4=1 << 20, wide_levels=1)),
+          ("W2", dict(deep_levels=2, wide_levels=2)), ("W3", dict(deep_levels=2, wide_levels=3))]
+if len(sys.argv) > 4:
+    shapes = [x for x in shapes if x[0] in sys.argv[4].split(",")]
 for dep in depths:
     nodes = ops.cpu().pfsp_bfs_level(m.native, m.host_lb, best, dep)
     if len(nodes) == 0:

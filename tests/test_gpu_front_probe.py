@@ -46,6 +46,8 @@ def start(model, best, target, take=None):
     ({"fuse_max": 0}, ["one_level"]),
     ({"deep_levels": 2}, ["child_parallel", "one_level"]),
     ({"deep_levels": 4, "deep_per3": 64, "deep_per4": 16, "max_parents": 1 << 13}, ["child_parallel", "thread_per_node"]),
+    ({"wide_levels": 3}, ["one_level", "thread_per_node"]),
+    ({"wide_levels": 1}, ["one_level", "child_parallel"]),
 ])
 def test_front_probe_ta014_every_shape(cfg, kinds):
     model = PfspModel(14, 1)
