@@ -105,7 +105,7 @@ def _rank_spec(a, world: int = 1) -> dict:
     # The host's cores are shared by the ranks of THIS node (LOCAL_WORLD_SIZE), not by
     # the whole job: on several nodes the global WORLD_SIZE would under-provision them.
     local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    cpu = max(1, _cpu_worker_threads(local) // max(1, local)) if a.C == 1 else 0
+    cpu = max(1, _cpu_worker_threads(local, a.streams) // max(1, local)) if a.C == 1 else 0
     return {"problem": "pfsp", "inst": a.inst, "lb": a.lb, "ub": a.ub, "backend": "gpu",
             "engine": {"max_parents": a.max_parents, "ring_bytes": int(a.ring_gb * (1 << 30)),
                        "streams": max(1, a.streams)},
@@ -114,14 +114,16 @@ def _rank_spec(a, world: int = 1) -> dict:
             "pin": bool(a.pin)}
 
 
-def _cpu_worker_threads(n_gpus: int) -> int:
+def _cpu_worker_threads(n_gpus: int, engines_per_gpu: int = 1) -> int:
     """ref pfsp_multigpu_cuda.c:61-69: nprocs/deviceCount threads per GPU, one of which
-    drives the GPU; here the CPU threads of all GPUs form one multithreaded worker."""
+    drives the GPU; here the CPU threads of all GPUs form one multithreaded worker.
+    Every engine has a host thread of its own (--streams engines per GPU), so the CPU
+    worker gets the cores left after those: no oversubscribed host."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, n - n_gpus)
+    return max(1, n - n_gpus * max(1, engines_per_gpu))
 
 
 def _pfsp_single_process(a, model) -> int:
@@ -135,7 +137,7 @@ def _pfsp_single_process(a, model) -> int:
     if devices and max(devices) >= gpu_count():
         print("Execution Terminated. More GPU devices requested than the ones available")
         return 1
-    threads = _cpu_worker_threads(len(devices)) if a.C == 1 else 0
+    threads = _cpu_worker_threads(len(devices), a.streams) if a.C == 1 else 0
     print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, a.D, a.C, a.ws, 1, a.L, 2))
     opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * 2**30), cpu_batch=a.T,
                          cpu_threads=max(1, threads), streams=max(1, a.streams))

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -27,36 +28,76 @@ class CpuEngine final : public IEngine {
 
   CpuEngine(Problem prob, size_t batch, int threads) : prob_(std::move(prob)), batch_(std::max<size_t>(1, batch)),
                                                         threads_(std::max(1, threads)) {}
+  ~CpuEngine() override { join_bg(); }
 
   size_t node_bytes() const override { return sizeof(Node); }
-  size_t size() override { return pool_.size(); }
-  int best() override { return best_; }
-  void set_best(int b) override { best_ = b; }
-  void reset_counters() override { tree_ = sol_ = parents_ = launches_ = 0; }
-  void synchronize() override {}
+  size_t size() override {
+    join_bg();
+    return pool_.size();
+  }
+  int best() override {
+    join_bg();
+    return best_;
+  }
+  void set_best(int b) override {
+    join_bg();
+    best_ = b;
+  }
+  void reset_counters() override {
+    join_bg();
+    tree_ = sol_ = parents_ = launches_ = 0;
+  }
+  void synchronize() override { join_bg(); }
   uintptr_t stream() const override { return 0; }
   int device() const override { return -1; }
 
   void push_host(const void* nodes, size_t n) override {
+    join_bg();
     pool_.push_back_bulk_free(static_cast<const Node*>(nodes), n);
   }
-  void import_device(const void* src, size_t n) override { push_host(src, n); }
+  // (may run next to a batch in flight: the pool is locked, the batch's children join
+  // it when the batch ends)
+  void import_device(const void* src, size_t n) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    pool_.push_back_bulk_free(static_cast<const Node*>(src), n);
+  }
 
   // Oldest (bottom) nodes first, like the GPU engine's export.
   size_t pop_host(void* out, size_t max_n) override {
-    const size_t n = std::min(max_n, pool_.size());
-    Node tmp;
-    Node* dst = static_cast<Node*>(out);
-    for (size_t i = 0; i < n; ++i) {
-      pool_.pop_front_free(tmp);
-      dst[i] = tmp;
-    }
-    return n;
+    join_bg();
+    return pop_front_locked(out, max_n);
   }
-  size_t export_device(void* dst, size_t max_n) override { return pop_host(dst, max_n); }
+  // (may run next to a batch in flight, like the GPU engine's export from under a replay)
+  size_t export_device(void* dst, size_t max_n) override {
+    if (bg_.joinable()) ++overlapped_exports_;
+    return pop_front_locked(dst, max_n);
+  }
+
+  // ---- overlapped rounds (engine_api.hpp): one batch "in flight" on a host thread ----
+  void set_overlap(bool on) override {
+    overlap_ = on;
+    if (!on) join_bg();
+  }
+  bool in_flight() override { return bg_.joinable(); }
+  size_t size_known() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    return pool_.size() + bg_n_;
+  }
+  int best_known() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    return std::min(best_, pending_best_);
+  }
+  bool split_pending_known() override { return split_world_ > 1 && !split_done_; }
+  void offer_best(int b) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    pending_best_ = std::min(pending_best_, b);
+    if (!bg_.joinable() && pending_best_ < best_) best_ = pending_best_;
+  }
+  unsigned long long overlapped_exports() const { return overlapped_exports_; }
 
   // One "launch" expands up to `batch` parents from the top of the pool.
   long run(long max_launches, double max_seconds, size_t stop_below) override {
+    join_bg();  // a batch the previous (overlapped) run left in flight
     const double t0 = now_s();
     long launches = 0;
     if (split_world_ > 1 && !split_done_) {
@@ -69,12 +110,18 @@ class CpuEngine final : public IEngine {
     std::vector<Node> parents(batch_);
     while (!pool_.empty() && pool_.size() >= std::max<size_t>(stop_below, 1)) {
       if (max_launches >= 0 && launches >= max_launches) break;
-      if (max_seconds > 0 && now_s() - t0 >= max_seconds) break;
+      if (max_seconds > 0 && now_s() - t0 >= max_seconds) {
+        leave_one();
+        break;
+      }
       if (hook_) {
         int b = best_;
         const bool stop = hook_(pool_.size(), b);
         best_ = std::min(best_, b);
-        if (stop) break;
+        if (stop) {
+          leave_one();
+          break;
+        }
       }
       const size_t n = pool_.pop_back_bulk_free(1, batch_, parents.data(), 1);
       expand(parents.data(), n);
@@ -140,6 +187,7 @@ class CpuEngine final : public IEngine {
   }
 
   EngineStats stats() override {
+    join_bg();
     EngineStats s;
     s.tree = tree_;
     s.sol = sol_;
@@ -150,10 +198,62 @@ class CpuEngine final : public IEngine {
     s.best = best_;
     s.device_nodes = pool_.size();
     s.t_run = t_run_;
+    s.overlapped_exports = overlapped_exports_;
+    s.left_inflight = left_inflight_;
     return s;
   }
 
  private:
+  size_t pop_front_locked(void* out, size_t max_n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    const size_t n = std::min(max_n, pool_.size());
+    Node tmp;
+    Node* dst = static_cast<Node*>(out);
+    for (size_t i = 0; i < n; ++i) {
+      pool_.pop_front_free(tmp);
+      dst[i] = tmp;
+    }
+    return n;
+  }
+  // Overlapped rounds: with at least two batches pooled, one more batch goes to a host
+  // thread that expands it while the caller runs its round; its children, counts and
+  // incumbent join the engine when it ends (join_bg). Exports meanwhile take the pool's
+  // oldest nodes under the lock.
+  void leave_one() {
+    if (!overlap_ || bg_.joinable() || pool_.size() < 2 * batch_) return;
+    std::vector<Node> mine(batch_);
+    size_t n = 0;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      n = pool_.pop_back_bulk_free(1, batch_, mine.data(), 1);
+      bg_n_ = n;
+    }
+    mine.resize(n);
+    ++left_inflight_;
+    const int b0 = best_;
+    bg_ = std::thread([this, mine = std::move(mine), b0]() {
+      int b = b0;
+      u64 tr = 0, so = 0;
+      std::vector<Node> kids;
+      for (const Node& p : mine) prob_.decompose(p, b, tr, so, [&](const Node& c) { kids.push_back(c); });
+      std::lock_guard<std::mutex> lk(mu_);
+      pool_.push_back_bulk_free(kids.data(), kids.size());
+      tree_ += tr;
+      sol_ += so;
+      parents_ += mine.size();
+      ++launches_;
+      bg_best_ = b;
+      bg_n_ = 0;
+    });
+  }
+  void join_bg() {
+    if (!bg_.joinable()) return;
+    bg_.join();
+    std::lock_guard<std::mutex> lk(mu_);
+    best_ = std::min({best_, bg_best_, pending_best_});
+    bg_best_ = pending_best_ = 0x7fffffff;
+  }
+
   // Same contract as the device split: identical breadth-first expansion on every
   // rank until the pool holds split_min_ nodes, then a strided 1/world share;
   // ranks != 0 drop the replicated counts. A tree that dies out first is left to
@@ -214,6 +314,13 @@ class CpuEngine final : public IEngine {
   size_t arm_min_ = 1, split_min_ = 1;
   bool split_done_ = false;
   ProgressHook hook_;
+  // overlapped rounds (leave_one / join_bg)
+  std::mutex mu_;
+  std::thread bg_;
+  size_t bg_n_ = 0;
+  int bg_best_ = 0x7fffffff, pending_best_ = 0x7fffffff;
+  bool overlap_ = false;
+  unsigned long long overlapped_exports_ = 0, left_inflight_ = 0;
 };
 
 // CPU engine that keeps its PFSP instance alive (for callers that build the
@@ -236,6 +343,12 @@ class OwningCpuEngine final : public IEngine {
   void set_split(int r, int w, size_t mp) override { eng_.set_split(r, w, mp); }
   bool split_pending() override { return eng_.split_pending(); }
   void set_progress_hook(ProgressHook h) override { eng_.set_progress_hook(std::move(h)); }
+  void set_overlap(bool on) override { eng_.set_overlap(on); }
+  bool in_flight() override { return eng_.in_flight(); }
+  size_t size_known() override { return eng_.size_known(); }
+  int best_known() override { return eng_.best_known(); }
+  bool split_pending_known() override { return eng_.split_pending_known(); }
+  void offer_best(int b) override { eng_.offer_best(b); }
   double pool_weight(const std::vector<double>& w) override { return eng_.pool_weight(w); }
   void set_best(int b) override { eng_.set_best(b); }
   int best() override { return eng_.best(); }

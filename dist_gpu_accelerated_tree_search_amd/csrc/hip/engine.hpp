@@ -26,6 +26,7 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "../core/engine_api.hpp"
@@ -800,6 +801,10 @@ class DeviceEngine final : public IEngine, public DeviceResource {
       unsigned spins = 0;
       while (__atomic_load_n(seq, __ATOMIC_ACQUIRE) < want) {
         __builtin_ia32_pause();
+        // back off after ~50 us of spinning: yield the core now and then, so several
+        // engines per GPU plus CPU workers on a full host do not starve each other
+        // (sched_yield returns at once when no other thread wants the core)
+        if (spins > 4096 && (spins & 63) == 0) std::this_thread::yield();
         if ((++spins & 1023) == 0) {
           const hipError_t q = hipEventQuery(graph_done_[m]);
           if (q == hipSuccess) {

@@ -264,3 +264,24 @@ def test_in_search_split_queens_cpu():
     spec = {"problem": "nqueens", "N": 11, "backend": "cpu", "dist": {"split": True}}
     res = spawn_local(3, solve_rank, (spec,), timeout=300)
     assert (res[0]["tree"], res[0]["sol"]) == (166925, 2680)
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_overlapped_rounds_keep_golden_tree(overlap):
+    # overlapped rounds (DistConfig.overlap): a rank's slice may end with one batch still
+    # expanding on a host thread (CpuEngine::leave_one, the CPU twin of a GPU replay left
+    # in flight); the status all-gather, the plan and the transfers — exports take the
+    # pool's oldest nodes from under the running batch — happen meanwhile. Every Step-1
+    # node starts on rank 0, so rank 0 donates during rounds that overlap its batches.
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu", "engine": {"cpu_batch": 512},
+            "dist": {"start_on": 0, "split": False, "init_per_rank": 25, "overlap": overlap}}
+    res = spawn_local(3, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == GOLD
+    ov = res[0]["extra"]["overlapped_rounds"]
+    assert len(ov) == 3
+    if overlap:
+        assert sum(ov) > 0, ov
+        assert sum(res[0]["extra"]["received_nodes"]) > 0
+    else:
+        assert sum(ov) == 0
