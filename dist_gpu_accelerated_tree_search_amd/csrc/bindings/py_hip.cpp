@@ -310,9 +310,9 @@ PYBIND11_MODULE(_tts_hip, m) {
       },
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("nodes"), py::arg("best"),
       py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 16, py::arg("fuse_max") = 1 << 30,
-      py::arg("deep_levels") = 4, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("local_steps") = 4,
+      py::arg("deep_levels") = 2, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("local_steps") = 4,
       py::arg("cap") = 1u << 22, py::arg("split_rank") = 0, py::arg("split_world") = 1, py::arg("split_min") = 0,
-      py::arg("wide_levels") = 2,
+      py::arg("wide_levels") = 1,
       "A complete front-kernel engine solve from these (front-layout) nodes with probe records on: every child "
       "bound of every iteration shape checked against the host oracle (counts of records and mismatches).");
   m.def(
@@ -346,8 +346,8 @@ PYBIND11_MODULE(_tts_hip, m) {
       },
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("nodes"), py::arg("best"),
       py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 19, py::arg("fuse_max") = 1 << 30,
-      py::arg("deep_levels") = 4, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("reps") = 20,
-      py::arg("wide_levels") = 2,
+      py::arg("deep_levels") = 2, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("reps") = 20,
+      py::arg("wide_levels") = 1,
       "Time one front-kernel iteration over this window: min / median ms, and the per-workgroup phase stamps.");
   m.def(
       "queens_labels",

@@ -28,10 +28,13 @@ struct EngineConfig {
   int iters_first = 18;                  // first replay after begin(): covers a 20-job tree in one graph
   int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
   int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
-  int deep_levels = 4;                   // fused iterations: at most this many tree levels (kernels that have them)
+  // (measured on ta014, one MI355X: 3 / 4-level narrow chunks and 2 / 3-level wide ones
+  // were 1-2 % / 2-19 % slower than two levels — the extra in-workgroup levels run
+  // serially behind one another at ~6 us each, what a new iteration kernel also costs)
+  int deep_levels = 2;                   // fused iterations: at most this many tree levels (kernels that have them)
   int deep_per3 = 8;                     // ... 3 levels when a workgroup takes at most this many parents
   int deep_per4 = 2;                     // ... 4 levels when a workgroup takes at most this many parents
-  int wide_levels = 2;                   // wide windows (<= one parent per thread): levels per iteration (< 2: off)
+  int wide_levels = 1;                   // wide windows (<= one parent per thread): levels per iteration (< 2: off)
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };

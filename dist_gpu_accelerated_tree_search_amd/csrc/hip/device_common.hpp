@@ -35,6 +35,18 @@ struct alignas(128) CtlI32 {
   int pad[31];
 };
 
+// Resident workgroups per CU of a kBlock kernel: the occupancy API's count capped by
+// what the SGPR file holds. A SIMD has 800 SGPRs and a wave takes ceil(sgpr / 16) * 16
+// + 16 of them; the search kernels allocate 106 (the compiler's default without a
+// waves-per-EU target), i.e. 6 waves per SIMD = 6 workgroups per CU, while the API
+// reports one more (measured on MI355X: with 7 per CU in the grid, 256 workgroups
+// started one workgroup lifetime late). Grids larger than the resident count only add
+// that serialisation.
+constexpr int kSgprResidentCap = 6;
+inline int resident_blocks(int api_blocks_per_cu, int cap = kSgprResidentCap) {
+  return api_blocks_per_cu < cap ? api_blocks_per_cu : cap;
+}
+
 // Workgroup exclusive scan of one int per thread (kBlock threads).
 // `scratch` needs kBlock/kWave ints of LDS. Returns the exclusive prefix; *total
 // receives the block sum. Contains __syncthreads().

@@ -49,7 +49,7 @@ struct PfspTraits {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_expand_kernel<NJ, M, LBK>, dev::kBlock, 0) !=
         hipSuccess)
       return 1;
-    return n;
+    return dev::resident_blocks(n);  // 106 SGPRs: 6 resident per CU
   }
 };
 

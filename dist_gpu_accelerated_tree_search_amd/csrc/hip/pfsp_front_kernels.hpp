@@ -106,9 +106,11 @@ struct FrontSmem {
   // multi-level chunks: two levels of nodes (ping-pong), each node with its remain
   // (unscheduled work per machine, packed u16 pairs), and the child offsets of the
   // level being expanded
-  uint4 lvl[2][G::CAP][G::VPN];
-  uint32_t rlv[2][G::CAP][G::HW];
-  int coff[G::CAP];
+  // (two CAP-node buffers, lvl[b * CAP + i]; a wide two-level chunk uses both as one
+  // 2 * CAP-node level)
+  uint4 lvl[2 * G::CAP][G::VPN];
+  uint32_t rlv[2 * G::CAP][G::HW];
+  int coff[2 * G::CAP];
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -475,7 +477,7 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
                 "chunk output must fit its slot region");
   static_assert(kBlock * (G::NJ - 1) + (G::WLMAX - 1) * G::CAP * (G::NJ - 1) <= G::SLOT,
                 "wide chunk output must fit its slot region");
-  static_assert(G::CAP <= kBlock && G::BPF_CP <= G::CAP, "one thread per staged node");
+  static_assert(2 * G::CAP <= kBlock && G::BPF_CP <= G::CAP, "one thread per staged node");
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   Node* const bout = pa.buf[(t & 1) ^ 1];
@@ -498,23 +500,27 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
       if (tid < n0) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
       front_remain<M>(sm, w, r2);
       const bool last = L == 1;
+      // the first LDS level: both buffers when it is also the last one expanded (two
+      // levels), else buffer 1 (buffer 0 then takes the level after it)
+      const int cap1 = L == 2 ? 2 * G::CAP : G::CAP;
+      const int base1 = L == 2 ? 0 : G::CAP;
       const int nn = front_expand_tp_regs<M>(
           a, sm, w, r2, best, nleaf,
           [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {
-            if (!last && i < G::CAP) {
-              front_store<M>(&sm.lvl[1][i][0], c);
+            if (!last && i < cap1) {
+              front_store<M>(&sm.lvl[base1 + i][0], c);
 #pragma unroll
-              for (int h = 0; h < G::HW; ++h) sm.rlv[1][i][h] = r[h];
+              for (int h = 0; h < G::HW; ++h) sm.rlv[base1 + i][h] = r[h];
             } else {
-              front_store<M>(out + (last ? i : i - G::CAP) * G::VPN, c);
+              front_store<M>(out + (last ? i : i - cap1) * G::VPN, c);
             }
           },
           kDbgOne);
       __syncthreads();
-      o = last ? nn : max(0, nn - G::CAP);
-      n = last ? 0 : min(nn, G::CAP);
+      o = last ? nn : max(0, nn - cap1);
+      n = last ? 0 : min(nn, cap1);
       inner = n;
-      cur = 1;
+      cur = L == 2 ? 0 : 1;
       lev0 = 1;
       if (first) front_stamp(a, 4);
     } else {
@@ -523,10 +529,10 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
         // < 65536, pfsp_front_ok), by the thread that stages it
         uint32_t w[G::NW], r2[G::HW];
         front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
-        front_store<M>(&sm.lvl[0][tid][0], w);
+        front_store<M>(&sm.lvl[tid][0], w);
         front_remain<M>(sm, w, r2);
 #pragma unroll
-        for (int h = 0; h < G::HW; ++h) sm.rlv[0][tid][h] = r2[h];
+        for (int h = 0; h < G::HW; ++h) sm.rlv[tid][h] = r2[h];
       }
       __syncthreads();
     }
@@ -536,16 +542,18 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
       const int nx = cur ^ 1;
       auto store = [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {
         if (!last && i < G::CAP) {
-          front_store<M>(&sm.lvl[nx][i][0], c);
+          front_store<M>(&sm.lvl[nx * G::CAP + i][0], c);
 #pragma unroll
-          for (int h = 0; h < G::HW; ++h) sm.rlv[nx][i][h] = r[h];
+          for (int h = 0; h < G::HW; ++h) sm.rlv[nx * G::CAP + i][h] = r[h];
         } else {
           front_store<M>(out + (o + (last ? i : i - G::CAP)) * G::VPN, c);
         }
       };
-      const int T = front_child_offsets<M>(sm, sm.lvl[cur], n);
-      const int nn = T > a.cp_max ? front_expand_tp<M>(a, sm, sm.lvl[cur], sm.rlv[cur], n, best, nleaf, store)
-                                  : front_expand_cp<M>(a, sm, sm.lvl[cur], sm.rlv[cur], n, T, best, nleaf, store);
+      const uint4(*src)[G::VPN] = sm.lvl + cur * G::CAP;
+      const uint32_t(*rsrc)[G::HW] = sm.rlv + cur * G::CAP;
+      const int T = front_child_offsets<M>(sm, src, n);
+      const int nn = T > a.cp_max ? front_expand_tp<M>(a, sm, src, rsrc, n, best, nleaf, store)
+                                  : front_expand_cp<M>(a, sm, src, rsrc, n, T, best, nleaf, store);
       __syncthreads();  // the next level is visible; this level's buffer is free
       o += last ? nn : max(0, nn - G::CAP);
       n = last ? 0 : min(nn, G::CAP);

@@ -30,7 +30,7 @@ struct QueensTraits {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::queens_expand_kernel, dev::kBlock, 0) != hipSuccess)
       return 1;
-    return n;
+    return dev::resident_blocks(n);  // 106 SGPRs: 6 resident per CU
   }
 };
 

@@ -6,6 +6,7 @@ Stamps (pfsp_front_kernels.hpp front_stamp): 0 entry, 1 pool_begin done, 2 table
 LDS, multi-level: 3 parents staged, 4..7 after level 0..3, 8 chunk done; one level:
 4 bounds done, 5 scan done, 6 children stored; 15 workgroup exit.
 """
+import os
 import sys
 
 import numpy as np
@@ -22,6 +23,8 @@ m = PfspModel(inst, lb)
 H = ops.require_gpu(0)
 best = m.best_known
 depths = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else list(range(2, 20))
+# rank share of an S-rank split: every S-th node of the level (TTS_PROBE_SHARE=S)
+share = int(os.environ.get("TTS_PROBE_SHARE", "1"))
 shapes = [("one", dict(fuse_max=0)), ("L2", dict(deep_levels=2, wide_levels=1)),
           ("L3", dict(deep_levels=3, deep_per3=1 << 20, wide_levels=1)),
           ("L4", dict(deep_levels=4, deep_per3=1 << 20, deep_per4=1 << 20, wide_levels=1)),
@@ -29,7 +32,7 @@ shapes = [("one", dict(fuse_max=0)), ("L2", dict(deep_levels=2, wide_levels=1)),
 if len(sys.argv) > 4:
     shapes = [x for x in shapes if x[0] in sys.argv[4].split(",")]
 for dep in depths:
-    nodes = ops.cpu().pfsp_bfs_level(m.native, m.host_lb, best, dep)
+    nodes = ops.cpu().pfsp_bfs_level(m.native, m.host_lb, best, dep)[::share]
     if len(nodes) == 0:
         continue
     depth = np.bincount(nodes[:, 0])

@@ -42,12 +42,13 @@ def start(model, best, target, take=None):
 
 
 @pytest.mark.parametrize("cfg,kinds", [
-    ({}, ["child_parallel", "thread_per_node", "one_level"]),
+    ({}, ["child_parallel", "one_level"]),
+    ({"deep_levels": 4}, ["child_parallel", "thread_per_node", "one_level"]),
     ({"fuse_max": 0}, ["one_level"]),
     ({"deep_levels": 2}, ["child_parallel", "one_level"]),
     ({"deep_levels": 4, "deep_per3": 64, "deep_per4": 16, "max_parents": 1 << 13}, ["child_parallel", "thread_per_node"]),
     ({"wide_levels": 3}, ["one_level", "thread_per_node"]),
-    ({"wide_levels": 1}, ["one_level", "child_parallel"]),
+    ({"wide_levels": 2}, ["one_level", "thread_per_node"]),
 ])
 def test_front_probe_ta014_every_shape(cfg, kinds):
     model = PfspModel(14, 1)
