@@ -79,9 +79,10 @@ class CpuEngine final : public IEngine {
     if (!on) join_bg();
   }
   bool in_flight() override { return bg_.joinable(); }
+  // (the pool without the batch in flight: exports can always take half of it)
   size_t size_known() override {
     std::lock_guard<std::mutex> lk(mu_);
-    return pool_.size() + bg_n_;
+    return std::max<size_t>(pool_.size(), bg_n_ ? 1 : 0);
   }
   int best_known() override {
     std::lock_guard<std::mutex> lk(mu_);

@@ -349,10 +349,12 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     }
   }
   bool in_flight() override { return !inflight_.empty(); }
+  // With a replay in flight: what can be exported from under it (export_ahead) — the
+  // ring part the running replays cannot reach — so a plan built on this size never
+  // asks for more than the pool can give without waiting; at least 1 (the replay is work).
   size_t size_known() override {
     if (inflight_.empty()) return size();
-    const size_t known = dev_total() - export_pending_ + spill_.size() + refill_n_;
-    return std::max<size_t>(known, 1);
+    return std::max<size_t>(exportable_ahead(), 1);
   }
   int best_known() override { return std::min(h_ctl_->best.v, pending_best_); }
   unsigned long long tree_known() override {
@@ -735,13 +737,16 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   // window of margin) are read by no replay; they were written by completed ones. The
   // copy runs on the transfer stream now; the nodes leave the host shadow's stack when
   // the replays have completed (commit_export).
-  bool export_ahead(Node* dst, size_t n) {
-    if (ahead_n_ || refill_n_ || !resv_.empty()) return false;
+  size_t exportable_ahead() const {
+    if (ahead_n_ || refill_n_ || !resv_.empty()) return 0;
     size_t k = 0;
     for (int x : inflight_k_) k += static_cast<size_t>(x);
     const size_t safe = (k + 1) * cfg_.max_parents;
     const size_t stack = dev_stack() - export_pending_;
-    if (stack < n + safe) return false;
+    return stack > safe ? stack - safe : 0;
+  }
+  bool export_ahead(Node* dst, size_t n) {
+    if (exportable_ahead() < n) return false;
     const size_t start = (h_ctl_->bot + export_pending_) & (cap_ - 1);
     const size_t first = std::min(n, cap_ - start);
     TTS_HIP_CHECK(hipMemcpyAsync(dst, d_ring_ + start, first * sizeof(Node), hipMemcpyDeviceToDevice, xfer_));

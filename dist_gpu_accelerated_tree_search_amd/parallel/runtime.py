@@ -211,7 +211,8 @@ def _native_options(cfg: DistConfig, engine, comm: Comm, window: int | None):
     opts = dict(needy_below=needy, donor_min=donor, steal_cap=cfg.steal_cap, slice_min=cfg.slice_min_s,
                 slice_max=cfg.slice_max_s, intra=bool(cfg.ws and share), inter=bool(cfg.L and share),
                 local_world=comm.topo.local_world, early_rounds=cfg.early_rounds, max_rounds=cfg.max_rounds,
-                time_limit=float(cfg.time_limit_s), live_best=bool(cfg.live_best), overlap=bool(cfg.overlap),
+                time_limit=float(cfg.time_limit_s), live_best=bool(cfg.live_best),
+                overlap=bool(cfg.overlap) and env.get("TTS_OVERLAP", "1") != "0",
                 trace_incumbent=bool(cfg.trace_incumbent),
                 checkpoint_every=cfg.checkpoint_every if cfg.checkpoint_dir else 0,
                 watchdog_s=float(cfg.watchdog_s or float(env.get("TTS_WATCHDOG_S", "0") or 0)),
