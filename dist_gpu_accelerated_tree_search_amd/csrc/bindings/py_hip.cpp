@@ -273,9 +273,10 @@ PYBIND11_MODULE(_tts_hip, m) {
       "pfsp_front_probe",
       [](int jobs, int machines, std::vector<int> p, int lb, U8 nodes, int best, int device, size_t max_parents,
          int fuse_max, int deep_levels, int deep_per3, int deep_per4, int local_steps, unsigned cap, int split_rank,
-         int split_world, size_t split_min, int wide_levels) {
+         int split_world, size_t split_min, int wide_levels, int local_min) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p));
         EngineConfig c;
+        c.local_min = local_min;
         c.device = device;
         c.max_parents = max_parents;
         c.ring_bytes = size_t(1) << 30;
@@ -312,7 +313,7 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 16, py::arg("fuse_max") = 1 << 30,
       py::arg("deep_levels") = 2, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("local_steps") = 4,
       py::arg("cap") = 1u << 22, py::arg("split_rank") = 0, py::arg("split_world") = 1, py::arg("split_min") = 0,
-      py::arg("wide_levels") = 1,
+      py::arg("wide_levels") = 1, py::arg("local_min") = -1,
       "A complete front-kernel engine solve from these (front-layout) nodes with probe records on: every child "
       "bound of every iteration shape checked against the host oracle (counts of records and mismatches).");
   m.def(

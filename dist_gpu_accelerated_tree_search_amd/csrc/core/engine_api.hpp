@@ -28,6 +28,9 @@ struct EngineConfig {
   int iters_first = 18;                  // first replay after begin(): covers a 20-job tree in one graph
   int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
   int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
+  // local DFS iterations once the pool holds this many parents (-1: the kernel's default,
+  // Traits::kLocalMin; 0: four grid-filling windows)
+  int local_min = -1;
   // (measured on ta014, one MI355X: 3 / 4-level narrow chunks and 2 / 3-level wide ones
   // were 1-2 % / 2-19 % slower than two levels — the extra in-workgroup levels run
   // serially behind one another at ~6 us each, what a new iteration kernel also costs)

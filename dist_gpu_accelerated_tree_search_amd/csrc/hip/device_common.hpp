@@ -78,5 +78,11 @@ __device__ inline u64 lanemask_lt() {
   return lane == 0 ? 0ull : (~0ull >> (kWave - lane));
 }
 
+// Packed u16 pairs (v_pk_add_u16 / v_pk_max_u16 on ext_vector_type(2)): two
+// independent 16-bit chains per VALU op where every value provably fits 16 bits.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ inline uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
 }  // namespace dev
 }  // namespace tts

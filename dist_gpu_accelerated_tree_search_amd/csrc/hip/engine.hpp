@@ -123,8 +123,6 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (const char* f = std::getenv("TTS_FUSE_MAX")) pa.fuse_max = std::max(0, std::atoi(f));
     pa.local_steps = std::min(cfg_.local_steps, Traits::kLocalSteps);
     if (const char* f = std::getenv("TTS_LOCAL_STEPS")) pa.local_steps = std::min(std::max(0, std::atoi(f)), Traits::kLocalSteps);
-    pa.local_min = 0;
-    if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
     // multi-level fused iterations (kernels with LMAX > 2): 3 levels up to deep_per[0]
     // parents per workgroup, 4 up to deep_per[1]; TTS_DEEP_LEVELS / _P3 / _P4 for A/B runs
     pa.deep_levels = cfg_.deep_levels;
@@ -136,6 +134,13 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     pa.wide_levels = cfg_.wide_levels;
     if (const char* f = std::getenv("TTS_WIDE_LEVELS")) pa.wide_levels = std::atoi(f);
     grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, resident)));
+    // the kernel's local DFS threshold only with a parent window of at least a resident
+    // grid of chunks: a narrower window cannot take in what a local iteration leaves (up to
+    // a slot region per workgroup), and a 4-rank ta008 solve on 2^14-parent windows lost
+    // its balance that way (tests/test_gpu_distributed.py skewed start)
+    pa.local_min = cfg_.local_min >= 0 ? cfg_.local_min
+                   : (cfg_.max_parents >= resident * Traits::kParentsPerChunk ? Traits::kLocalMin : 0);
+    if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known
     // pool spans a whole parent window (spec_min_). Queuing it earlier

@@ -33,6 +33,7 @@ struct PfspTraits {
   static constexpr int kChildrenPerChunk = G::SLOT;  // slot region per chunk
   static constexpr int kMaxChildren = NJ;            // children per parent (one level)
   static constexpr int kLocalSteps = G::LT;
+  static constexpr int kLocalMin = 0;
   static constexpr int kMaxChunks = G::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, LBK>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
@@ -63,6 +64,11 @@ struct PfspFrontTraits {
   static constexpr int kChildrenPerChunk = G::SLOT;
   static constexpr int kMaxChildren = G::NJ;
   static constexpr int kLocalSteps = G::LT;
+  // local DFS from 16K-parent windows: the wide levels of a 20-job tree take up to
+  // local_steps levels per dependent kernel (ta014 -u 1, one MI355X: 0.234 -> 0.221 ms;
+  // rank shares of 2/4/8-way splits 9-12 % faster; ta021 unchanged — its pool is a
+  // backlog anyway; 4K-parent windows were slower again: profiles/r4/local_min.txt)
+  static constexpr int kLocalMin = 16384;
   static constexpr int kMaxChunks = G::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);

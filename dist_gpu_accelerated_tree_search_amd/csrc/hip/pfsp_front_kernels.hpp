@@ -170,47 +170,99 @@ __device__ inline void front_dbg(const PfspFrontArgs<M>& a, int kind, const uint
   for (int h = 0; h < G::HW; ++h) r[2 + G::NW + h] = rp[h];
 }
 
-// Bounds of every child of the parent held in w: emit(j, lb) for each unscheduled job j.
+// Packed u16 pairs: two children's chains per VALU op (v_pk_max_u16 / v_pk_add_u16; the
+// p rows of the pair interleaved by one v_perm_b32 per machine). Every value of the chain
+// stays below 65536: the instance's processing times sum below it (pfsp_front_ok) and a
+// bound never exceeds a schedule's makespan.
+
+// Bounds of the children appending the jobs of `rest` to a parent whose front / remain +
+// tail are fb[m] / rb[m] (each value in both halves): emit(j, lb) per job, ascending,
+// two jobs per pass (ref add_front_and_bound, c_bound_simple.c:219-244).
 template <int M, class Emit>
-__device__ inline void front_parent(const PfspFrontArgs<M>& a, const FrontSmem<M>& sm,
-                                    const uint32_t (&w)[FrontGeom<M>::NW], Emit emit, int kind = kDbgOne) {
-  const uint32_t rest = w[1];
-  int f[M], r[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    f[m] = front_of<M>(w, m);
-    r[m] = a.min_tails[m];
-  }
-  for (uint32_t x = rest; x; x &= x - 1) {
-    int pr[M];
-    front_row<M>(sm.ptab[__builtin_ctz(x)], pr);
-#pragma unroll
-    for (int m = 0; m < M; ++m) r[m] += pr[m];
-  }
+__device__ inline void front_bounds_x2(const FrontSmem<M>& sm, const uint32_t (&fb)[M], const uint32_t (&rb)[M],
+                                       uint32_t rest, Emit emit) {
+  constexpr int HW = FrontGeom<M>::HW;
+#ifdef TTS_AB_UNPACKED
   for (uint32_t x = rest; x; x &= x - 1) {
     const int j = __builtin_ctz(x);
     int pr[M];
     front_row<M>(sm.ptab[j], pr);
-    int lb = f[0] + r[0];
-    int tt = f[0] + pr[0];
+    int lb = static_cast<int>(fb[0] & 0xffffu) + static_cast<int>(rb[0] & 0xffffu);
+    int tt = static_cast<int>(fb[0] & 0xffffu) + pr[0];
 #pragma unroll
     for (int m = 1; m < M; ++m) {
-      const int sv = max(tt, f[m]);
-      lb = max(lb, sv + r[m]);
+      const int sv = max(tt, static_cast<int>(fb[m] & 0xffffu));
+      lb = max(lb, sv + static_cast<int>(rb[m] & 0xffffu));
       tt = sv + pr[m];
-    }
-    if (a.dbg_rec) {
-      uint32_t rp[FrontGeom<M>::HW];
-#pragma unroll
-      for (int h = 0; h < FrontGeom<M>::HW; ++h) {
-        const uint32_t lo = static_cast<uint32_t>(r[2 * h] - a.min_tails[2 * h]);
-        const uint32_t hi = 2 * h + 1 < M ? static_cast<uint32_t>(r[2 * h + 1] - a.min_tails[2 * h + 1]) : 0u;
-        rp[h] = lo | (hi << 16);
-      }
-      front_dbg<M>(a, kind, w, rp, j, lb);
     }
     emit(j, lb);
   }
+  return;
+#endif
+  for (uint32_t x = rest; x;) {
+    const int j1 = __builtin_ctz(x);
+    x &= x - 1;
+    const bool two = x != 0;
+    const int j2 = two ? __builtin_ctz(x) : j1;
+    x &= x - 1;
+    const uint32_t* r1 = reinterpret_cast<const uint32_t*>(sm.ptab[j1]);
+    const uint32_t* r2 = reinterpret_cast<const uint32_t*>(sm.ptab[j2]);
+    uint32_t a[HW], b[HW];
+#pragma unroll
+    for (int h = 0; h < HW; ++h) {
+      a[h] = r1[h];
+      b[h] = r2[h];
+    }
+    u16x2 lb = as_u16x2(fb[0]) + as_u16x2(rb[0]);
+    u16x2 tt = as_u16x2(fb[0]) + as_u16x2(__builtin_amdgcn_perm(b[0], a[0], 0x05040100u));
+#pragma unroll
+    for (int m = 1; m < M; ++m) {
+      const u16x2 pm = as_u16x2(__builtin_amdgcn_perm(b[m >> 1], a[m >> 1], (m & 1) ? 0x07060302u : 0x05040100u));
+      const u16x2 sv = __builtin_elementwise_max(tt, as_u16x2(fb[m]));
+      lb = __builtin_elementwise_max(lb, sv + as_u16x2(rb[m]));
+      tt = sv + pm;
+    }
+    const uint32_t l = as_u32(lb);
+    emit(j1, static_cast<int>(l & 0xffffu));
+    if (two) emit(j2, static_cast<int>(l >> 16));
+  }
+}
+
+// fb / rb of a parent: its front (words of w) and its packed remain rp plus the tails
+template <int M>
+__device__ inline void front_broadcast(const PfspFrontArgs<M>& a, const uint32_t (&w)[FrontGeom<M>::NW],
+                                       const uint32_t (&rp)[FrontGeom<M>::HW], uint32_t (&fb)[M], uint32_t (&rb)[M]) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    fb[m] = static_cast<uint32_t>(front_of<M>(w, m)) * 0x10001u;
+    rb[m] = (((rp[m >> 1] >> ((m & 1) * 16)) & 0xffffu) + static_cast<uint32_t>(a.min_tails[m])) * 0x10001u;
+  }
+}
+
+// The packed remain of the node in w: the sum of its unscheduled jobs' p rows.
+template <int M>
+__device__ inline void front_remain(const FrontSmem<M>& sm, const uint32_t (&w)[FrontGeom<M>::NW],
+                                    uint32_t (&r2)[FrontGeom<M>::HW]) {
+#pragma unroll
+  for (int h = 0; h < FrontGeom<M>::HW; ++h) r2[h] = 0;
+  for (uint32_t x = w[1]; x; x &= x - 1) {
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[__builtin_ctz(x)]);
+#pragma unroll
+    for (int h = 0; h < FrontGeom<M>::HW; ++h) r2[h] += row[h];
+  }
+}
+
+// Bounds of every child of the parent held in w: emit(j, lb) for each unscheduled job j.
+template <int M, class Emit>
+__device__ inline void front_parent(const PfspFrontArgs<M>& a, const FrontSmem<M>& sm,
+                                    const uint32_t (&w)[FrontGeom<M>::NW], Emit emit, int kind = kDbgOne) {
+  uint32_t rp[FrontGeom<M>::HW], fb[M], rb[M];
+  front_remain<M>(sm, w, rp);
+  front_broadcast<M>(a, w, rp, fb, rb);
+  front_bounds_x2<M>(sm, fb, rb, w[1], [&](int j, int lb) {
+    if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
+    emit(j, lb);
+  });
 }
 
 // Child of the parent in w that appends job j: depth + 1, j removed from the set, and
@@ -376,24 +428,9 @@ __device__ inline int front_expand_tp_regs(const PfspFrontArgs<M>& a, FrontSmem<
   int nsurv = 0;
   const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
   {
-    int f[M], r[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      f[m] = front_of<M>(w, m);
-      r[m] = static_cast<int>((rp[m >> 1] >> ((m & 1) * 16)) & 0xffffu) + a.min_tails[m];
-    }
-    for (uint32_t x = w[1]; x; x &= x - 1) {
-      const int j = __builtin_ctz(x);
-      int pr[M];
-      front_row<M>(sm.ptab[j], pr);
-      int lb = f[0] + r[0];
-      int tt = f[0] + pr[0];
-#pragma unroll
-      for (int m = 1; m < M; ++m) {
-        const int sv = max(tt, f[m]);
-        lb = max(lb, sv + r[m]);
-        tt = sv + pr[m];
-      }
+    uint32_t fb[M], rb[M];
+    front_broadcast<M>(a, w, rp, fb, rb);
+    front_bounds_x2<M>(sm, fb, rb, w[1], [&](int j, int lb) {
       if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
       if (leaf) {
         ++nleaf;
@@ -402,7 +439,7 @@ __device__ inline int front_expand_tp_regs(const PfspFrontArgs<M>& a, FrontSmem<
         ++nsurv;
         surv |= 1u << j;
       }
-    }
+    });
   }
   int tot = 0;
   int idx = block_exclusive_scan(nsurv, sm.scan, &tot);
@@ -444,19 +481,6 @@ __device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
     for (int h = 0; h < HW; ++h) rp[h] = rem[tid][h];
   }
   return front_expand_tp_regs<M>(a, sm, w, rp, best, nleaf, store);
-}
-
-// The packed remain of the node in w: the sum of its unscheduled jobs' p rows.
-template <int M>
-__device__ inline void front_remain(const FrontSmem<M>& sm, const uint32_t (&w)[FrontGeom<M>::NW],
-                                    uint32_t (&r2)[FrontGeom<M>::HW]) {
-#pragma unroll
-  for (int h = 0; h < FrontGeom<M>::HW; ++h) r2[h] = 0;
-  for (uint32_t x = w[1]; x; x &= x - 1) {
-    const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[__builtin_ctz(x)]);
-#pragma unroll
-    for (int h = 0; h < FrontGeom<M>::HW; ++h) r2[h] += row[h];
-  }
 }
 
 // Multi-level chunk (fused iterations): the chunk's v.bp parents go to LDS with their

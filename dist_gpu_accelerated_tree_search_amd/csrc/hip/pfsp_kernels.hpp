@@ -634,9 +634,7 @@ __device__ inline void lb2_walk_pipe(const uint4* rq, int ndouble, const u64 (&m
 // value is a path length through the p matrix (host check lb2_pk_ok: (jobs + machines
 // - 1) x max p < 65536). Job sets of NW > 1 words (100-job instances) pick the word
 // of the record's job first (one 64-bit select per word and child).
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
-__device__ inline uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// (u16x2 helpers: device_common.hpp)
 
 template <int NW>
 __device__ inline void lb2_step2(uint32_t x, uint32_t y, const u64 (&mav)[NW], const u64 (&mbv)[NW], uint32_t& t0,

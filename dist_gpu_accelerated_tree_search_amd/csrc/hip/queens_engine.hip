@@ -15,6 +15,7 @@ struct QueensTraits {
   static constexpr int kChildrenPerChunk = S::MAXCH;
   static constexpr int kMaxChildren = S::MAXCH / S::BP;
   static constexpr int kLocalSteps = 1;
+  static constexpr int kLocalMin = 0;
   static constexpr int kMaxChunks = S::MAXCHUNKS;
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL(dev::queens_expand_kernel, dim3(grid), dim3(dev::kBlock), 0, s, a, t);

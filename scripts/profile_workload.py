@@ -2,6 +2,10 @@
 import sys
 sys.path.insert(0, ".")
 import torch  # noqa: F401
+import os
+if os.environ.get("TTS_DUMP_MAPS"):  # the process mappings at exit (resolve a crash PC from a finalizer)
+    import atexit
+    atexit.register(lambda: open(os.environ["TTS_DUMP_MAPS"], "w").write(open("/proc/self/maps").read()))
 from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel, QueensModel, solve_engine
 
 which = sys.argv[1] if len(sys.argv) > 1 else "ta014"

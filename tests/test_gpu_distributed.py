@@ -48,6 +48,7 @@ def test_gpu_skewed_start_is_balanced_through_device_staging():
         assert (r["tree"], r["sol"], r["best"]) == (113458723, 808498, 1206)
     per = [w["tree"] for w in res[0]["workers"]]
     mean = sum(per) / len(per)
+    print("per-rank tree", per, "rounds", res[0]["extra"]["rounds"])
     assert max(per) <= 1.5 * mean, per
     assert res[0]["extra"]["needy_below"] == 4096 and res[0]["extra"]["donor_min"] == 16384
     assert sum(r["comm"]["device_transfers"] for r in res) > 0

@@ -41,19 +41,23 @@ def start(model, best, target, take=None):
     return nodes, t, s, b
 
 
+# (local_min 0: local DFS only on a backlog of four grid windows, so the wide levels run
+# one level per kernel; the default local_min takes them local on a window of at least a
+# resident grid of chunks, as the headline's 2^19)
 @pytest.mark.parametrize("cfg,kinds", [
-    ({}, ["child_parallel", "one_level"]),
-    ({"deep_levels": 4}, ["child_parallel", "thread_per_node", "one_level"]),
-    ({"fuse_max": 0}, ["one_level"]),
-    ({"deep_levels": 2}, ["child_parallel", "one_level"]),
+    ({}, ["child_parallel", "local_dfs"]),
+    ({"local_min": 0}, ["child_parallel", "one_level"]),
+    ({"deep_levels": 4, "local_min": 0}, ["child_parallel", "thread_per_node", "one_level"]),
+    ({"fuse_max": 0}, ["one_level", "local_dfs"]),
+    ({"deep_levels": 2}, ["child_parallel", "local_dfs"]),
     ({"deep_levels": 4, "deep_per3": 64, "deep_per4": 16, "max_parents": 1 << 13}, ["child_parallel", "thread_per_node"]),
-    ({"wide_levels": 3}, ["one_level", "thread_per_node"]),
-    ({"wide_levels": 2}, ["one_level", "thread_per_node"]),
+    ({"wide_levels": 3, "local_min": 0}, ["one_level", "thread_per_node"]),
+    ({"wide_levels": 2, "local_min": 0}, ["one_level", "thread_per_node"]),
 ])
 def test_front_probe_ta014_every_shape(cfg, kinds):
     model = PfspModel(14, 1)
     nodes, t0, s0, best = start(model, 1377, 25)
-    r = probe(model, nodes, best, cap=1 << 25, **cfg)
+    r = probe(model, nodes, best, cap=1 << 25, **{"max_parents": 1 << 19, **cfg})  # the headline window
     check(r, kinds)
     assert (r["tree"] + t0, r["sol"] + s0, r["best"]) == (2573652, 2648, 1377)
 
