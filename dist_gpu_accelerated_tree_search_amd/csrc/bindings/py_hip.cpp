@@ -125,7 +125,11 @@ PYBIND11_MODULE(_tts_hip, m) {
   m.def("release_all", &DeviceResource::release_all,
         "Free the device resources of every live engine and RCCL transport (also run at exit).");
   m.def("live_resources", &DeviceResource::live_count);
-  py::module_::import("atexit").attr("register")(py::cpp_function([]() { DeviceResource::release_all(); }));
+  py::module_::import("atexit").attr("register")(py::cpp_function([]() {
+    if (const char* e = std::getenv("TTS_EXIT_MODE"))  // profiler exit-crash diagnosis (scripts/profile_workload.py)
+      if (std::string(e) == "keep") return;
+    DeviceResource::release_all();
+  }));
   m.def("device_pci_bus_id", &device_pci_bus_id);
   m.def("device_cpus", &device_cpus, "CPUs of the NUMA node closest to the GPU (empty if unknown).");
 
@@ -319,10 +323,13 @@ PYBIND11_MODULE(_tts_hip, m) {
   m.def(
       "pfsp_front_time",
       [](int jobs, int machines, std::vector<int> p, int lb, U8 nodes, int best, int device, size_t max_parents,
-         int fuse_max, int deep_levels, int deep_per3, int deep_per4, int reps, int wide_levels) {
+         int fuse_max, int deep_levels, int deep_per3, int deep_per4, int reps, int wide_levels, int local_min,
+         int local_steps) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p));
         EngineConfig c;
         c.device = device;
+        c.local_min = local_min;
+        c.local_steps = local_steps;
         c.max_parents = max_parents;
         c.fuse_max = fuse_max;
         c.deep_levels = deep_levels;
@@ -348,7 +355,7 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("nodes"), py::arg("best"),
       py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 19, py::arg("fuse_max") = 1 << 30,
       py::arg("deep_levels") = 2, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("reps") = 20,
-      py::arg("wide_levels") = 1,
+      py::arg("wide_levels") = 1, py::arg("local_min") = 0, py::arg("local_steps") = 4,
       "Time one front-kernel iteration over this window: min / median ms, and the per-workgroup phase stamps.");
   m.def(
       "queens_labels",

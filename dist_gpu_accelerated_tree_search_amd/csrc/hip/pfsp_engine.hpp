@@ -595,6 +595,7 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   pa.max_chunks = static_cast<int>(max_chunks);
   pa.fuse_max = cfg.fuse_max;
   pa.local_steps = std::min(cfg.local_steps, G::LT);
+  pa.local_min = std::max(0, cfg.local_min);
   pa.deep_levels = cfg.deep_levels;
   pa.deep_per[0] = cfg.deep_per3;
   pa.deep_per[1] = cfg.deep_per4;

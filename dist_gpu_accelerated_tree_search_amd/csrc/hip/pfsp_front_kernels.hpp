@@ -182,23 +182,26 @@ template <int M, class Emit>
 __device__ inline void front_bounds_x2(const FrontSmem<M>& sm, const uint32_t (&fb)[M], const uint32_t (&rb)[M],
                                        uint32_t rest, Emit emit) {
   constexpr int HW = FrontGeom<M>::HW;
-#ifdef TTS_AB_UNPACKED
-  for (uint32_t x = rest; x; x &= x - 1) {
-    const int j = __builtin_ctz(x);
-    int pr[M];
-    front_row<M>(sm.ptab[j], pr);
-    int lb = static_cast<int>(fb[0] & 0xffffu) + static_cast<int>(rb[0] & 0xffffu);
-    int tt = static_cast<int>(fb[0] & 0xffffu) + pr[0];
+  // 20 machines: one child per pass (same-box A/B on ta021 LB1_d: packed pairs 9.82 s,
+  // one child 9.31 s; on ta014's 10 machines the pairs win, 0.2245 -> 0.2209 ms:
+  // profiles/r4/packed_bounds_ab.txt)
+  if constexpr (M > 10) {
+    for (uint32_t x = rest; x; x &= x - 1) {
+      const int j = __builtin_ctz(x);
+      int pr[M];
+      front_row<M>(sm.ptab[j], pr);
+      int lb = static_cast<int>(fb[0] & 0xffffu) + static_cast<int>(rb[0] & 0xffffu);
+      int tt = static_cast<int>(fb[0] & 0xffffu) + pr[0];
 #pragma unroll
-    for (int m = 1; m < M; ++m) {
-      const int sv = max(tt, static_cast<int>(fb[m] & 0xffffu));
-      lb = max(lb, sv + static_cast<int>(rb[m] & 0xffffu));
-      tt = sv + pr[m];
+      for (int m = 1; m < M; ++m) {
+        const int sv = max(tt, static_cast<int>(fb[m] & 0xffffu));
+        lb = max(lb, sv + static_cast<int>(rb[m] & 0xffffu));
+        tt = sv + pr[m];
+      }
+      emit(j, lb);
     }
-    emit(j, lb);
+    return;
   }
-  return;
-#endif
   for (uint32_t x = rest; x;) {
     const int j1 = __builtin_ctz(x);
     x &= x - 1;
@@ -652,6 +655,7 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
       // pushes visible to the next step's pops (workgroup scope), and room left for
       // one more full step
       __syncthreads();
+      if (ch == static_cast<int>(blockIdx.x) && s < 4) front_stamp(a, 4 + s);
       if (top + kBlock * G::NJ > G::SLOT || top > v.cap) break;
     }
     int leaves = 0;
@@ -706,6 +710,7 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
   front_stamp(a, 2);
   if (v.local) {
     front_local<M>(a, sm, v, t, best);
+    front_stamp(a, 15);
     return;
   }
   if (v.fused) {

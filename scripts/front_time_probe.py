@@ -4,7 +4,8 @@ shape (one level, 2/3/4-level chunks), with per-workgroup phase stamps.
     python scripts/front_time_probe.py [inst] [lb]
 Stamps (pfsp_front_kernels.hpp front_stamp): 0 entry, 1 pool_begin done, 2 tables in
 LDS, multi-level: 3 parents staged, 4..7 after level 0..3, 8 chunk done; one level:
-4 bounds done, 5 scan done, 6 children stored; 15 workgroup exit.
+4 bounds done, 5 scan done, 6 children stored; local DFS (LOC): 4..7 after step 0..3;
+15 workgroup exit.
 """
 import os
 import sys
@@ -28,7 +29,8 @@ share = int(os.environ.get("TTS_PROBE_SHARE", "1"))
 shapes = [("one", dict(fuse_max=0)), ("L2", dict(deep_levels=2, wide_levels=1)),
           ("L3", dict(deep_levels=3, deep_per3=1 << 20, wide_levels=1)),
           ("L4", dict(deep_levels=4, deep_per3=1 << 20, deep_per4=1 << 20, wide_levels=1)),
-          ("W2", dict(deep_levels=2, wide_levels=2)), ("W3", dict(deep_levels=2, wide_levels=3))]
+          ("W2", dict(deep_levels=2, wide_levels=2)), ("W3", dict(deep_levels=2, wide_levels=3)),
+          ("LOC", dict(local_min=1, local_steps=4)), ("LOC2", dict(local_min=1, local_steps=2))]
 if len(sys.argv) > 4:
     shapes = [x for x in shapes if x[0] in sys.argv[4].split(",")]
 for dep in depths:

@@ -109,7 +109,8 @@ elif which.startswith("spill014"):  # spill014[:ring_MB]: ta014 LB1 solved to th
     eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 10, ring_bytes=ring))
     ts = []
     for rep in range(4):
-        eng.set_trace(rep == 3)  # the last solve records the replay / copy timeline
+        # the last solve records the replay / copy timeline (TTS_EXIT_MODE=notrace: none)
+        eng.set_trace(rep == 3 and os.environ.get("TTS_EXIT_MODE") != "notrace")
         t0 = time.perf_counter()
         eng.begin(nodes, int(best))
         eng.run()
@@ -120,6 +121,9 @@ elif which.startswith("spill014"):  # spill014[:ring_MB]: ta014 LB1 solved to th
     print(which, f"{len(nodes)} begin nodes, capacity {st['capacity']} nodes: {min(ts[:3]) * 1e3:.2f} ms per solve "
           f"(best of 3 untraced), spilled {st['spilled']} refilled {st['refilled']} (last solve), "
           f"pinned MB {st['pinned_bytes'] >> 20}")
+    if os.environ.get("TTS_EXIT_MODE") == "notrace":
+        del eng
+        raise SystemExit(0)
     tr = eng.trace()
     import numpy as np
     g = tr[tr[:, 0] == 0][:, 1:]
@@ -132,6 +136,15 @@ elif which.startswith("spill014"):  # spill014[:ring_MB]: ta014 LB1 solved to th
         print(f"  {name}: {len(c)} copies (enqueue-to-complete spans), {tot:.3f} ms, {ov:.3f} ms "
               f"({100 * ov / tot if tot else 0:.0f} %) while a graph replay ran")
     print(f"  replays: {len(g)}, {float((g[:, 1] - g[:, 0]).sum()):.3f} ms; traced solve {ts[3] * 1e3:.2f} ms")
+    # exit-crash diagnosis under rocprofv3 --memory-copy-trace (profiles/r4/spill/README.md):
+    # TTS_EXIT_MODE=sleep waits before the engine is released, =keep never releases it
+    mode = os.environ.get("TTS_EXIT_MODE", "")
+    if mode == "sleep":
+        time.sleep(1.0)
+    if mode == "keep":
+        import builtins
+        builtins._tts_keep = eng
+        raise SystemExit(0)
     del eng
     raise SystemExit(0)
 elif which == "queens":
