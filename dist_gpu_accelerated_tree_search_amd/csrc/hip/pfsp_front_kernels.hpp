@@ -107,10 +107,19 @@ struct FrontSmem {
   // (unscheduled work per machine, packed u16 pairs), and the child offsets of the
   // level being expanded
   // (two CAP-node buffers, lvl[b * CAP + i]; a wide two-level chunk uses both as one
-  // 2 * CAP-node level)
-  uint4 lvl[2 * G::CAP][G::VPN];
-  uint32_t rlv[2 * G::CAP][G::HW];
-  int coff[2 * G::CAP];
+  // 2 * CAP-node level). Local DFS chunks use the same bytes for the nodes the next step
+  // pops (front_local).
+  union {
+    struct {
+      uint4 lvl[2 * G::CAP][G::VPN];
+      uint32_t rlv[2 * G::CAP][G::HW];
+      int coff[2 * G::CAP];
+    };
+    struct {
+      uint4 stage[kBlock][G::VPN];
+      uint32_t stage_r[kBlock][G::HW];  // their remains (packed u16 pairs)
+    };
+  };
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
@@ -256,6 +265,19 @@ __device__ inline void front_remain(const FrontSmem<M>& sm, const uint32_t (&w)[
 }
 
 // Bounds of every child of the parent held in w: emit(j, lb) for each unscheduled job j.
+// (the parent's packed remain rp given)
+template <int M, class Emit>
+__device__ inline void front_parent_r(const PfspFrontArgs<M>& a, const FrontSmem<M>& sm,
+                                      const uint32_t (&w)[FrontGeom<M>::NW], const uint32_t (&rp)[FrontGeom<M>::HW],
+                                      Emit emit, int kind) {
+  uint32_t fb[M], rb[M];
+  front_broadcast<M>(a, w, rp, fb, rb);
+  front_bounds_x2<M>(sm, fb, rb, w[1], [&](int j, int lb) {
+    if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
+    emit(j, lb);
+  });
+}
+
 template <int M, class Emit>
 __device__ inline void front_parent(const PfspFrontArgs<M>& a, const FrontSmem<M>& sm,
                                     const uint32_t (&w)[FrontGeom<M>::NW], Emit emit, int kind = kDbgOne) {
@@ -288,6 +310,19 @@ __device__ inline void front_child(const FrontSmem<M>& sm, const uint32_t (&w)[F
   for (int m = 1; m < M; ++m) {
     ft = max(ft, root ? 0 : front_of<M>(w, m)) + pr[m];
     c[2 + (m >> 1)] |= static_cast<uint32_t>(ft) << ((m & 1) * 16);
+  }
+}
+
+// (store(i, child words, job) for the i-th surviving child of w)
+template <int M, class Store>
+__device__ inline void front_emit_to(const FrontSmem<M>& sm, const uint32_t (&w)[FrontGeom<M>::NW], uint32_t surv,
+                                     Store store) {
+  for (int i = 0; surv; ++i) {
+    const int j = __builtin_ctz(surv);
+    surv &= surv - 1;
+    uint32_t c[FrontGeom<M>::NW];
+    front_child<M>(sm, w, j, c);
+    store(i, c, j);
   }
 }
 
@@ -618,9 +653,12 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     Node* const stk = bout + static_cast<size_t>(ch) * G::SLOT;
-    int top = 0, pushed = 0, nleaf = 0;
+    // nst: how many of the nodes on top of the stack are held in sm.stage (the previous
+    // step's last children, exactly the ones this step pops) instead of the slot region
+    int top = 0, pushed = 0, nleaf = 0, nst = 0;
     for (int s = 0; s < v.steps; ++s) {
-      uint32_t w[G::NW];
+      uint32_t w[G::NW], rp[G::HW];
+      bool have_r = false;  // rp carried with a staged node
 #pragma unroll
       for (int i = 0; i < G::NW; ++i) w[i] = 0;
       if (s == 0) {
@@ -629,14 +667,32 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
       } else {
         if (top == 0) break;  // uniform
         const int npop = min(top, kBlock);
-        if (tid < npop) front_load<M>(stk + (top - npop + tid), w);
+        if (tid < npop) {
+          const int k = tid - (npop - nst);
+          if (k >= 0) {
+#pragma unroll
+            for (int q = 0; q < G::VPN; ++q) {
+              const uint4 x = sm.stage[k][q];
+              w[4 * q] = x.x;
+              w[4 * q + 1] = x.y;
+              w[4 * q + 2] = x.z;
+              w[4 * q + 3] = x.w;
+            }
+#pragma unroll
+            for (int h = 0; h < G::HW; ++h) rp[h] = sm.stage_r[k][h];
+            have_r = true;
+          } else {
+            front_load<M>(stk + (top - npop + tid), w);
+          }
+        }
         top -= npop;
       }
       uint32_t surv = 0;
       int nsurv = 0;
       const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-      front_parent<M>(
-          a, sm, w,
+      if (!have_r) front_remain<M>(sm, w, rp);
+      front_parent_r<M>(
+          a, sm, w, rp,
           [&](int j, int lb) {
             if (leaf) {
               ++nleaf;
@@ -649,14 +705,32 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
           kDbgLocal);
       int tot = 0;
       const int off = block_exclusive_scan(nsurv, sm.scan, &tot);
-      front_emit<M>(sm, w, surv, reinterpret_cast<uint4*>(stk + top + off));
-      top += tot;
+      // will another step run? then the children it pops (the last min(top, kBlock)
+      // pushed) stay in LDS and skip the slot region's store / load round trip
+      const int tnew = top + tot;
+      const bool more = s + 1 < v.steps && tnew > 0 && !(tnew + kBlock * G::NJ > G::SLOT || tnew > v.cap);
+      nst = more ? min(tot, min(tnew, kBlock)) : 0;
+      const int lo = tot - nst;
+      uint4* const dst = reinterpret_cast<uint4*>(stk + top);
+      // (the scan's barrier: every thread holds its popped node in registers by now)
+      front_emit_to<M>(sm, w, surv, [&](int i, const uint32_t (&c)[G::NW], int j) {
+        const int o = off + i;
+        if (o >= lo) {
+          front_store<M>(&sm.stage[o - lo][0], c);
+          const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
+#pragma unroll
+          for (int h = 0; h < G::HW; ++h) sm.stage_r[o - lo][h] = rp[h] - row[h];  // the child's remain
+        } else {
+          front_store<M>(dst + o * G::VPN, c);
+        }
+      });
+      top = tnew;
       pushed += tot;
       // pushes visible to the next step's pops (workgroup scope), and room left for
       // one more full step
       __syncthreads();
       if (ch == static_cast<int>(blockIdx.x) && s < 4) front_stamp(a, 4 + s);
-      if (top + kBlock * G::NJ > G::SLOT || top > v.cap) break;
+      if (!more) break;
     }
     int leaves = 0;
     (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
