@@ -374,11 +374,16 @@ __device__ inline int front_child_offsets(FrontSmem<M>& sm, const uint4 (*src)[F
   return T;
 }
 
+// Children a level keeps: all of them, except in a rank split's level (keep(node, job)).
+struct FrontKeepAll {
+  __device__ bool operator()(int, int) const { return true; }
+};
+
 // (T children, offsets in sm.coff: front_child_offsets)
-template <int M, class Store>
+template <int M, class Store, class Keep = FrontKeepAll>
 __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const uint4 (*src)[FrontGeom<M>::VPN],
                                       const uint32_t (*rem)[FrontGeom<M>::HW], int n, int T, int best, int& nleaf,
-                                      Store store) {
+                                      Store store, Keep keep = {}, int kind = kDbgCp) {
   using G = FrontGeom<M>;
   constexpr int HW = G::HW;
   const int tid = threadIdx.x;
@@ -429,12 +434,13 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
         lb = max(lb, sv + rm(m));
         tt = sv + pm(m);
       }
-      if (a.dbg_rec) front_dbg<M>(a, kDbgCp, w, rp, j, lb);
+      if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
+      const bool kp = keep(lo, j);
       if (static_cast<int>(w[0] & 0xffu) + 1 == a.jobs) {
-        ++nleaf;
+        nleaf += kp;
         if (lb < best) atomicMin(&a.pool.ctl->best.v, lb);
       } else {
-        surv = lb < best;
+        surv = kp && lb < best;
       }
     }
     int tot = 0;
@@ -456,10 +462,10 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
 // path: fewer instructions per child than front_expand_cp (no parent search, one node
 // load per parent), and the serial loop is short once most lanes hold a node.
 // (the node and its packed remain in registers; w = 0 for a thread without a node)
-template <int M, class Store>
+template <int M, class Store, class Keep = FrontKeepAll>
 __device__ inline int front_expand_tp_regs(const PfspFrontArgs<M>& a, FrontSmem<M>& sm,
                                            const uint32_t (&w)[FrontGeom<M>::NW], const uint32_t (&rp)[FrontGeom<M>::HW],
-                                           int best, int& nleaf, Store store, int kind = kDbgTp) {
+                                           int best, int& nleaf, Store store, int kind = kDbgTp, Keep keep = {}) {
   using G = FrontGeom<M>;
   constexpr int HW = G::HW;
   uint32_t surv = 0;
@@ -470,10 +476,11 @@ __device__ inline int front_expand_tp_regs(const PfspFrontArgs<M>& a, FrontSmem<
     front_broadcast<M>(a, w, rp, fb, rb);
     front_bounds_x2<M>(sm, fb, rb, w[1], [&](int j, int lb) {
       if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
+      const bool kp = keep(static_cast<int>(threadIdx.x), j);
       if (leaf) {
-        ++nleaf;
+        nleaf += kp;
         if (lb < best) atomicMin(&a.pool.ctl->best.v, lb);
-      } else if (lb < best) {
+      } else if (kp && lb < best) {
         ++nsurv;
         surv |= 1u << j;
       }
@@ -494,10 +501,10 @@ __device__ inline int front_expand_tp_regs(const PfspFrontArgs<M>& a, FrontSmem<
   return tot;
 }
 
-template <int M, class Store>
+template <int M, class Store, class Keep = FrontKeepAll>
 __device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm,
                                       const uint4 (*src)[FrontGeom<M>::VPN], const uint32_t (*rem)[FrontGeom<M>::HW],
-                                      int n, int best, int& nleaf, Store store) {
+                                      int n, int best, int& nleaf, Store store, Keep keep = {}, int kind = kDbgTp) {
   using G = FrontGeom<M>;
   constexpr int HW = G::HW;
   const int tid = threadIdx.x;
@@ -518,7 +525,7 @@ __device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
 #pragma unroll
     for (int h = 0; h < HW; ++h) rp[h] = rem[tid][h];
   }
-  return front_expand_tp_regs<M>(a, sm, w, rp, best, nleaf, store);
+  return front_expand_tp_regs<M>(a, sm, w, rp, best, nleaf, store, kind, keep);
 }
 
 // Multi-level chunk (fused iterations): the chunk's v.bp parents go to LDS with their
@@ -614,8 +621,15 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
       const uint4(*src)[G::VPN] = sm.lvl + cur * G::CAP;
       const uint32_t(*rsrc)[G::HW] = sm.rlv + cur * G::CAP;
       const int T = front_child_offsets<M>(sm, src, n);
-      const int nn = T > a.cp_max ? front_expand_tp<M>(a, sm, src, rsrc, n, best, nleaf, store)
-                                  : front_expand_cp<M>(a, sm, src, rsrc, n, T, best, nleaf, store);
+      // the first level of a rank split's iteration keeps this rank's children only
+      // (split_keep of the parent's window position and the job, as the one-level split)
+      const bool split_lev = v.split && lev == 0;
+      const u64 gbase = g0;
+      auto keep = [&](int p, int j) { return !split_lev || split_keep(v, gbase + static_cast<u64>(p), j); };
+      const int nn = T > a.cp_max
+                         ? front_expand_tp<M>(a, sm, src, rsrc, n, best, nleaf, store, keep, split_lev ? kDbgSplit : kDbgTp)
+                         : front_expand_cp<M>(a, sm, src, rsrc, n, T, best, nleaf, store, keep,
+                                              split_lev ? kDbgSplit : kDbgCp);
       __syncthreads();  // the next level is visible; this level's buffer is free
       o += last ? nn : max(0, nn - G::CAP);
       n = last ? 0 : min(nn, G::CAP);

@@ -246,7 +246,10 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // pool past the parent window before the split.
   const bool fuse_armed = armed && !(v.B >= split_min) &&
                           v.B * static_cast<u64>(max(GROW2, 1)) <= static_cast<u64>(pa.max_parents) && GROW2 > 0;
-  v.fused = !v.local && BPF > 0 && (!armed || fuse_armed) &&
+  // (the split iteration itself is fused too when the kernel passes LMAX > 2: its first
+  // level keeps this rank's children, the second expands them)
+  const bool fuse_split = v.split && LMAX > 2 && GROW2 > 0;
+  v.fused = !v.local && BPF > 0 && (!armed || fuse_armed || fuse_split) &&
             v.B <= static_cast<u64>(min(pa.fuse_max, BPF * pa.max_chunks));
   int bp = BP;
   v.levels = v.fused ? 2 : 1;
@@ -254,9 +257,12 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     // up to BPF parents per two-level chunk, fewer when the window is narrower than the
     // grid: more workgroups share a narrow window (each with fewer serial passes). While
     // a split is armed the pool order must not depend on the grid (every rank deals the
-    // same frontier by position), so those chunks keep BPF parents.
-    const u64 per = (v.B + gridDim.x - 1) / gridDim.x;
-    bp = armed ? BPF : static_cast<int>(min(static_cast<u64>(BPF), max(per, 1ull)));
+    // same frontier by position): the window is then spread over a fixed 1024 chunks
+    // instead of the grid (chunk order, not workgroup order, lays out the output). Never
+    // more chunks than the count / slot arrays hold (max_chunks; the grid is within it).
+    const u64 spread = min(armed ? 1024ull : static_cast<u64>(gridDim.x), static_cast<u64>(pa.max_chunks));
+    const u64 per = (v.B + spread - 1) / spread;
+    bp = static_cast<int>(min(static_cast<u64>(BPF), max(per, 1ull)));
     // narrower windows go deeper: 3 or 4 levels per dependent kernel while a chunk's
     // levels stay in LDS (never while armed: the split must see the replicated levels)
     const int lmax = min(LMAX, pa.deep_levels);
