@@ -730,7 +730,11 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   // Nothing in flight: launch one replay and leave it running (returns true if launched).
   bool leave_one(size_t total) {
     if (!leave_ok(total) || !inflight_.empty()) return false;
-    const int gi = pick_graph(total, 0);
+    // a replay short enough that half of the pool stays exportable from under it
+    // (exportable_ahead): a donor still looks like one to the round's plan (a 4-rank
+    // skewed start lost its balance behind 48-iteration replays)
+    const size_t kmax = std::max<size_t>(6, total / 2 / cfg_.max_parents);
+    const int gi = pick_graph(total, 0, kmax);
     if (gi < 0) return false;
     launch_graph(gi);
     start_spill_ahead();
@@ -836,11 +840,13 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   // Largest graph whose worst-case ring growth (plus `extra` already in flight)
   // fits, no longer than the pool size suggests: 6 iterations while ramping up or
   // draining, more when the pool holds several parent windows.
-  int pick_graph(size_t total, size_t extra) const {
+  int pick_graph(size_t total, size_t extra, size_t kmax = SIZE_MAX) const {
     // right after begin(): one long replay (iters_first) — a graph boundary costs
     // ~50 us of host sync + relaunch, an empty iteration ~4.5 us (profiles/r1/r1f)
     size_t want = fresh_ ? std::max<size_t>(6, static_cast<size_t>(cfg_.iters_first)) : 6;
-    while (want < static_cast<size_t>(cfg_.iters_large) && total >= (want / 6) * 2 * cfg_.max_parents) want *= 2;
+    while (want < static_cast<size_t>(cfg_.iters_large) && total >= (want / 6) * 2 * cfg_.max_parents &&
+           want * 2 <= kmax)
+      want *= 2;
     for (int i = static_cast<int>(ks_.size()) - 1; i >= 0; --i) {
       if (static_cast<size_t>(ks_[i]) > want && i > 0) continue;
       if (total + extra + reserved_ + static_cast<size_t>(ks_[i] + 1) * buf_nodes_ <= cap_) return i;
