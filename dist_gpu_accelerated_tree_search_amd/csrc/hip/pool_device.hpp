@@ -105,22 +105,63 @@ struct PoolSmem {
 };
 
 // Exclusive prefix of cnt[0..n) into pre[0..n] (pre[n] = total) by one workgroup.
+// Every count is loaded in one memory round trip (R predicated loads per thread,
+// unrolled, coalesced, staged in LDS), then each thread scans a contiguous run from
+// LDS: a loop of dependent global loads here cost ~3 round trips per kernel start
+// (s_waitcnt after every load pair in the ISA).
 template <int MAXCHUNKS>
 __device__ inline int build_prefix(const int* cnt, int n, PoolSmem<MAXCHUNKS>& ps) {
+  constexpr int R = (MAXCHUNKS + kBlock - 1) / kBlock;
+  const int tid = static_cast<int>(threadIdx.x);
+  int x[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = tid + k * kBlock;
+    x[k] = i < n ? cnt[i] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k)
+    if (tid + k * kBlock < n) ps.pre[tid + k * kBlock] = x[k];
+  __syncthreads();
   const int per = (n + kBlock - 1) / kBlock;
-  const int lo = min(n, static_cast<int>(threadIdx.x) * per);
+  const int lo = min(n, tid * per);
   const int hi = min(n, lo + per);
   int s = 0;
-  for (int i = lo; i < hi; ++i) s += cnt[i];
-  int total = 0;
-  int run = block_exclusive_scan(s, ps.scan, &total);
-  for (int i = lo; i < hi; ++i) {
-    ps.pre[i] = run;
-    run += cnt[i];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    x[k] = lo + k < hi ? ps.pre[lo + k] : 0;
+    s += x[k];
   }
+  int total = 0;
+  int run = block_exclusive_scan(s, ps.scan, &total);  // (its barrier: every run read)
+#pragma unroll
+  for (int k = 0; k < R; ++k)
+    if (lo + k < hi) {
+      ps.pre[lo + k] = run;
+      run += x[k];
+    }
   if (threadIdx.x == 0) ps.pre[n] = total;
   __syncthreads();
   return total;
+}
+
+// Sums over the per-chunk leaf words lcnt[0..n) (leaves, inner nodes) by one workgroup:
+// all loads in one round trip.
+template <int MAXCHUNKS>
+__device__ inline void sum_leaf_words(const int* lcnt, int n, int& lf, int& in) {
+  constexpr int R = (MAXCHUNKS + kBlock - 1) / kBlock;
+  int x[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = static_cast<int>(threadIdx.x) + k * kBlock;
+    x[k] = i < n ? lcnt[i] : 0;
+  }
+  lf = in = 0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    lf += lcnt_leaves(x[k]);
+    in += lcnt_inner(x[k]);
+  }
 }
 
 // Chunk holding buffered child li: the largest c < n with pre[c] <= li.
@@ -288,11 +329,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   if (blockIdx.x == 0) {
     // leaves evaluated by the previous iteration
     int lf = 0, in = 0;
-    for (int i = threadIdx.x; i < v.nch_in; i += kBlock) {
-      const int x = pa.lcnt[b_in][i];
-      lf += lcnt_leaves(x);
-      in += lcnt_inner(x);
-    }
+    sum_leaf_words<MAXCHUNKS>(pa.lcnt[b_in], v.nch_in, lf, in);
     int lf_total = 0, in_total = 0;
     (void)block_exclusive_scan(lf, ps.red, &lf_total);
     (void)block_exclusive_scan(in, ps.scan, &in_total);
@@ -453,11 +490,17 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   const int n = pa.ctl->slot[0].nch;
   const u64 seq = pa.ctl->seq + 1;
   int c = 0, l = 0, in = 0;
-  for (int i = threadIdx.x; i < n; i += kBlock) {
-    c += pa.cnt[b][i];
-    const int x = pa.lcnt[b][i];
-    l += lcnt_leaves(x);
-    in += lcnt_inner(x);
+  {
+    constexpr int R = (MAXCHUNKS + kBlock - 1) / kBlock;
+    int xc[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int i = static_cast<int>(threadIdx.x) + k * kBlock;
+      xc[k] = i < n ? pa.cnt[b][i] : 0;
+    }
+    sum_leaf_words<MAXCHUNKS>(pa.lcnt[b], n, l, in);
+#pragma unroll
+    for (int k = 0; k < R; ++k) c += xc[k];
   }
   int ct = 0, lt = 0, it = 0;
   (void)block_exclusive_scan(c, ps.scan, &ct);
