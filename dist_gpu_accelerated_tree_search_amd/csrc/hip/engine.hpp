@@ -141,6 +141,17 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     pa.local_min = cfg_.local_min >= 0 ? cfg_.local_min
                    : (cfg_.max_parents >= resident * Traits::kParentsPerChunk ? Traits::kLocalMin : 0);
     if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
+    pa.local_cap = 0;
+    if (const char* f = std::getenv("TTS_LOCAL_CAP")) pa.local_cap = std::max(0, std::atoi(f));
+    pa.local_deadline = 0;
+    // local DFS windows dealt strided (chunk ch takes window parents ch, ch + nchunks, ...):
+    // consecutive window nodes are one previous chunk's stack, siblings with alike survivor
+    // counts, so contiguous dealing handed some workgroups all the heavy subtrees (per-
+    // workgroup exit times track the first step's at r = 0.97; ta014 0.2305 -> 0.2182 ms,
+    // profiles/r4/local_stride_ab.txt)
+    pa.local_stride = 1;
+    if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);
+    if (const char* f = std::getenv("TTS_LOCAL_DEADLINE_US")) pa.local_deadline = std::max(0, std::atoi(f)) * 100;
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known
     // pool spans a whole parent window (spec_min_). Queuing it earlier

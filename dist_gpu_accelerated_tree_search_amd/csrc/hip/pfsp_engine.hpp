@@ -596,6 +596,10 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   pa.fuse_max = cfg.fuse_max;
   pa.local_steps = std::min(cfg.local_steps, G::LT);
   pa.local_min = std::max(0, cfg.local_min);
+  pa.local_cap = 0;
+  pa.local_deadline = 0;
+  pa.local_stride = 0;
+  if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);
   pa.deep_levels = cfg.deep_levels;
   pa.deep_per[0] = cfg.deep_per3;
   pa.deep_per[1] = cfg.deep_per4;

@@ -81,6 +81,9 @@ struct PoolArgs {
   int fuse_max;     // two-level iterations for windows of at most this many parents (0: off)
   int local_steps;  // > 1: local DFS iterations of up to this many steps per chunk (kernels that have them)
   int local_min;    // wide local DFS when the pool holds at least this many parents (0: 4 grid windows)
+  int local_cap;    // > 0: a local DFS chunk takes no further step once its stack holds more than this
+  int local_deadline;  // > 0: ... nor once this many wall-clock ticks (10 ns) have passed since its start
+  int local_stride;    // local DFS chunks take strided window parents (ch, ch + nchunks, ...)
   // multi-level iterations (kernels with LMAX > 2): a fused window of at most deep_per[0]
   // parents per workgroup is expanded 3 levels deep, of at most deep_per[1] 4 levels deep
   // (capped by deep_levels); 2 levels otherwise
@@ -271,7 +274,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // tree then also take a few local steps per dependent kernel)
   v.local = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= (pa.local_min > 0 ? lmin : max(lmin, full));
   v.steps = pa.local_steps;
-  v.cap = 0x7fffffff;
+  v.cap = pa.local_cap > 0 ? pa.local_cap : 0x7fffffff;
   if (v.local) v.B = min(v.B, full);
   v.nb = min(v.B, v.C);
   v.ns = v.B - v.nb;

@@ -57,6 +57,15 @@ for dep in depths:
             dt = col[ok] - base
             parts.append(f"s{k} {dt.mean():.2f}/{dt.max():.2f}")
             prev = k
+        if os.environ.get("TTS_PROBE_DETAIL"):  # exit time by XCD (workgroup i runs on XCD i % 8) and spread
+            xcd = np.arange(len(st)) % 8
+            by = [f"{ex[live & (xcd == x)].mean():.1f}/{ex[live & (xcd == x)].max():.1f}" for x in range(8)]
+            q = np.percentile(ex[live], [10, 50, 90, 99])
+            print(f"    exit by XCD (mean/max): {' '.join(by)} | p10/50/90/99 {q.round(1).tolist()}", flush=True)
+            if st[live, 4].any():
+                s0 = st[live, 4] - st[live, 2]
+                print(f"    step0 p10/50/90/99 {np.percentile(s0, [10, 50, 90, 99]).round(1).tolist()}; "
+                      f"corr(exit, step0) {np.corrcoef(ex[live], s0)[0, 1]:.2f}", flush=True)
         print(f"  {name:4s} {d['ms_min'] * 1e3:7.2f} us (median {d['ms_median'] * 1e3:.2f}) grid {d['grid']} "
               f"out chunks {d['nch_out']} | entry max {ent[live].max():.2f} exit mean {ex[live].mean():.2f} "
               f"max {ex[live].max():.2f} | " + " ".join(parts), flush=True)
