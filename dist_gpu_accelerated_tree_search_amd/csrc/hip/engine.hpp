@@ -144,11 +144,11 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     pa.local_cap = 0;
     if (const char* f = std::getenv("TTS_LOCAL_CAP")) pa.local_cap = std::max(0, std::atoi(f));
     pa.local_deadline = 0;
-    // local DFS windows dealt strided (chunk ch takes window parents ch, ch + nchunks, ...):
-    // consecutive window nodes are one previous chunk's stack, siblings with alike survivor
-    // counts, so contiguous dealing handed some workgroups all the heavy subtrees (per-
-    // workgroup exit times track the first step's at r = 0.97; ta014 0.2305 -> 0.2182 ms,
-    // profiles/r4/local_stride_ab.txt)
+    // local DFS windows dealt strided (chunk ch takes window parents ch, ch + nchunks, ...)
+    // below a backlog (pool_begin): consecutive window nodes are one previous chunk's stack,
+    // siblings with alike survivor counts, so contiguous dealing handed some workgroups all
+    // the heavy subtrees (per-workgroup exit times track the first step's at r = 0.97;
+    // ta014 0.2305 -> 0.2182 ms, rank shares -5..-9 %; profiles/r4/local_stride_ab.txt)
     pa.local_stride = 1;
     if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);
     if (const char* f = std::getenv("TTS_LOCAL_DEADLINE_US")) pa.local_deadline = std::max(0, std::atoi(f)) * 100;

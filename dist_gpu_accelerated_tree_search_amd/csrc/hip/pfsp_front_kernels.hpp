@@ -678,7 +678,7 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
 #pragma unroll
       for (int i = 0; i < G::NW; ++i) w[i] = 0;
       if (s == 0) {
-        const u64 gi = pa.local_stride ? static_cast<u64>(ch) + static_cast<u64>(tid) * static_cast<u64>(v.nchunks)
+        const u64 gi = v.stride ? static_cast<u64>(ch) + static_cast<u64>(tid) * static_cast<u64>(v.nchunks)
                                        : static_cast<u64>(ch) * v.bp + tid;
         if (tid < v.bp && gi < v.B) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
       } else {

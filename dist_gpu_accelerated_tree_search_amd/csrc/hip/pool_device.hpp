@@ -188,6 +188,7 @@ struct IterView {
   bool fused;         // multi-level iteration: chunks of BPF parents, `levels` tree levels deep
   int levels;         // fused iterations: tree levels expanded per chunk (2..LMAX)
   bool local;         // local DFS iteration: each chunk steps on its own stack
+  bool stride;        // local DFS: chunk ch takes window parents ch, ch + nchunks, ... (pa.local_stride)
   int bp;             // window parents per chunk
   int steps;          // local DFS: steps per chunk at most
   int cap;            // local DFS: no further step once the stack holds more than this
@@ -244,7 +245,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     // and leave — no table staging, no scans, no counter traffic
     v.C = v.B = v.nb = v.ns = v.L = v.Snew = v.bot = 0;
     v.nchunks = 0;
-    v.overflow = v.split = v.fused = v.local = v.armed = false;
+    v.overflow = v.split = v.fused = v.local = v.armed = v.stride = false;
     v.levels = 1;
     v.bp = BP;
     v.steps = v.cap = 0;
@@ -274,6 +275,9 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // tree then also take a few local steps per dependent kernel)
   v.local = LT > 1 && pa.local_steps > 1 && !armed && v.S + v.C >= (pa.local_min > 0 ? lmin : max(lmin, full));
   v.steps = pa.local_steps;
+  // strided local windows below a backlog of four grid windows (a tree's wide levels); on a
+  // backlog (ta021 LB1_d: millions of pooled nodes) contiguous dealing was faster
+  v.stride = v.local && pa.local_stride && v.S + v.C < 4 * full;
   v.cap = pa.local_cap > 0 ? pa.local_cap : 0x7fffffff;
   if (v.local) v.B = min(v.B, full);
   v.nb = min(v.B, v.C);
