@@ -151,6 +151,8 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     // ta014 0.2305 -> 0.2182 ms, rank shares -5..-9 %; profiles/r4/local_stride_ab.txt)
     pa.local_stride = 1;
     if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);
+    pa.local_wide_steps = 3;
+    if (const char* f = std::getenv("TTS_LOCAL_WIDE_STEPS")) pa.local_wide_steps = std::atoi(f);
     if (const char* f = std::getenv("TTS_LOCAL_DEADLINE_US")) pa.local_deadline = std::max(0, std::atoi(f)) * 100;
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known

@@ -84,6 +84,7 @@ struct PoolArgs {
   int local_cap;    // > 0: a local DFS chunk takes no further step once its stack holds more than this
   int local_deadline;  // > 0: ... nor once this many wall-clock ticks (10 ns) have passed since its start
   int local_stride;    // local DFS chunks take strided window parents (ch, ch + nchunks, ...)
+  int local_wide_steps;  // > 0: steps of a strided local window of at least 160 parents per workgroup
   // multi-level iterations (kernels with LMAX > 2): a fused window of at most deep_per[0]
   // parents per workgroup is expanded 3 levels deep, of at most deep_per[1] 4 levels deep
   // (capped by deep_levels); 2 levels otherwise
@@ -278,6 +279,10 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // strided local windows below a backlog of four grid windows (a tree's wide levels); on a
   // backlog (ta021 LB1_d: millions of pooled nodes) contiguous dealing was faster
   v.stride = v.local && pa.local_stride && v.S + v.C < 4 * full;
+  // wide strided windows (a tree's widest levels, full 256-node pops) take fewer steps: a
+  // step more there mostly lengthens the slowest workgroup (ta014 one rank: 3 steps 0.215
+  // vs 4 steps 0.219 ms; the narrower windows of 4- and 8-way rank shares keep 4)
+  if (v.stride && pa.local_wide_steps > 0 && min(v.B, full) >= 160ull * gridDim.x) v.steps = pa.local_wide_steps;
   v.cap = pa.local_cap > 0 ? pa.local_cap : 0x7fffffff;
   if (v.local) v.B = min(v.B, full);
   v.nb = min(v.B, v.C);
