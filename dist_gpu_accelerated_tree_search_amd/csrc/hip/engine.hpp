@@ -143,7 +143,6 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
     pa.local_cap = 0;
     if (const char* f = std::getenv("TTS_LOCAL_CAP")) pa.local_cap = std::max(0, std::atoi(f));
-    pa.local_deadline = 0;
     // local DFS windows dealt strided (chunk ch takes window parents ch, ch + nchunks, ...)
     // below a backlog (pool_begin): consecutive window nodes are one previous chunk's stack,
     // siblings with alike survivor counts, so contiguous dealing handed some workgroups all
@@ -153,7 +152,6 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);
     pa.local_wide_steps = 3;
     if (const char* f = std::getenv("TTS_LOCAL_WIDE_STEPS")) pa.local_wide_steps = std::atoi(f);
-    if (const char* f = std::getenv("TTS_LOCAL_DEADLINE_US")) pa.local_deadline = std::max(0, std::atoi(f)) * 100;
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known
     // pool spans a whole parent window (spec_min_). Queuing it earlier

@@ -103,7 +103,6 @@ struct FrontSmem {
   using G = FrontGeom<M>;
   uint16_t ptab[G::NJ][G::MS];
   int scan[kBlock / kWave];
-  int stop;  // local DFS deadline reached (thread 0 -> the workgroup)
   // multi-level chunks: two levels of nodes (ping-pong), each node with its remain
   // (unscheduled work per machine, packed u16 pairs), and the child offsets of the
   // level being expanded
@@ -666,7 +665,6 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
-  const unsigned long long t0 = wall_clock64();
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
     Node* const stk = bout + static_cast<size_t>(ch) * G::SLOT;
     // nst: how many of the nodes on top of the stack are held in sm.stage (the previous
@@ -725,12 +723,7 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
       // will another step run? then the children it pops (the last min(top, kBlock)
       // pushed) stay in LDS and skip the slot region's store / load round trip
       const int tnew = top + tot;
-      if (pa.local_deadline > 0 && tid == 0)
-        sm.stop = wall_clock64() - t0 > static_cast<unsigned long long>(pa.local_deadline);
-      if (pa.local_deadline > 0) __syncthreads();
-      const bool late = pa.local_deadline > 0 && sm.stop;
-      const bool more =
-          s + 1 < v.steps && tnew > 0 && !late && !(tnew + kBlock * G::NJ > G::SLOT || tnew > v.cap);
+      const bool more = s + 1 < v.steps && tnew > 0 && !(tnew + kBlock * G::NJ > G::SLOT || tnew > v.cap);
       nst = more ? min(tot, min(tnew, kBlock)) : 0;
       const int lo = tot - nst;
       uint4* const dst = reinterpret_cast<uint4*>(stk + top);

@@ -82,7 +82,6 @@ struct PoolArgs {
   int local_steps;  // > 1: local DFS iterations of up to this many steps per chunk (kernels that have them)
   int local_min;    // wide local DFS when the pool holds at least this many parents (0: 4 grid windows)
   int local_cap;    // > 0: a local DFS chunk takes no further step once its stack holds more than this
-  int local_deadline;  // > 0: ... nor once this many wall-clock ticks (10 ns) have passed since its start
   int local_stride;    // local DFS chunks take strided window parents (ch, ch + nchunks, ...)
   int local_wide_steps;  // > 0: steps of a strided local window of at least 160 parents per workgroup
   // multi-level iterations (kernels with LMAX > 2): a fused window of at most deep_per[0]
