@@ -152,6 +152,8 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);
     pa.local_wide_steps = 3;
     if (const char* f = std::getenv("TTS_LOCAL_WIDE_STEPS")) pa.local_wide_steps = std::atoi(f);
+    pa.local_narrow_steps = 6;
+    if (const char* f = std::getenv("TTS_LOCAL_NARROW_STEPS")) pa.local_narrow_steps = std::atoi(f);
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known
     // pool spans a whole parent window (spec_min_). Queuing it earlier
