@@ -58,6 +58,10 @@ def _pfsp_parser() -> argparse.ArgumentParser:
     ap.add_argument("--ring-gb", type=float, default=16.0)
     ap.add_argument("--streams", type=int, default=1,
                     help="engines per GPU, one stream and host thread each, run as one (large trees: 3)")
+    ap.add_argument("--comm", choices=["nccl", "gloo"], default="nccl",
+                    help="one process per GPU: node transfers over RCCL (default) or gloo (ranks may share a GPU)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="one process per GPU: put every rank on this device (tests; use with --comm gloo)")
     ap.add_argument("--json", default=None, help="append a JSON run record to this file")
     ap.add_argument("--csv-dir", default=".", help="directory of the CSV statistics files")
     ap.add_argument("--no-csv", action="store_true")
@@ -111,7 +115,7 @@ def _rank_spec(a, world: int = 1) -> dict:
                        "streams": max(1, a.streams)},
             "dist": {"m": a.m, "init_per_rank": a.m, "steal_cap": _steal_cap(a), "ws": bool(a.ws), "L": bool(a.L),
                      "slice_min_s": a.comm_period * 1e-3, "cpu_workers": max(0, cpu), "cpu_batch": a.T},
-            "pin": bool(a.pin)}
+            "pin": bool(a.pin), "comm": a.comm, **({} if a.device is None else {"device": a.device})}
 
 
 def _cpu_worker_threads(n_gpus: int, engines_per_gpu: int = 1) -> int:
@@ -209,7 +213,7 @@ def pfsp_main(argv: list[str]) -> int:
         from .ops import gpu_count
         from .parallel.launch import spawn_local
 
-        if a.D > gpu_count():
+        if (a.D > gpu_count()) if a.device is None else (a.device >= gpu_count()):
             print("Execution Terminated. More GPU devices requested than the ones available")
             return 1
         res = spawn_local(a.D, solve_rank, (spec,))[0]
@@ -304,9 +308,44 @@ def nqueens_main(argv: list[str]) -> int:
     return 0
 
 
+def _spawn_planned(argv: list[str]) -> bool:
+    """Will this command start one process per GPU itself (spawn_local)? That is -D N > 1
+    outside torchrun, for N-Queens always and for PFSP with -C 0 and no single-process
+    option. Parsed leniently: a wrong guess only costs (or skips) an early forkserver."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or len(argv) < 2:
+        return False
+
+    def opt(short: str, long: str, default: str) -> str:
+        v = default
+        for i, x in enumerate(argv):
+            if x in (short, long) and i + 1 < len(argv):
+                v = argv[i + 1]
+            elif x.startswith(long + "="):
+                v = x.split("=", 1)[1]
+        return v
+
+    try:
+        D = int(opt("-D", "--D", "1"))
+        C = int(opt("-C", "--C", "1"))
+    except ValueError:
+        return False
+    if D <= 1:
+        return False
+    if argv[0] == "nqueens":
+        return True
+    return C == 0 and "--single-process" not in argv and not any(x.startswith("--gpus-list") for x in argv)
+
+
 def main(argv: list[str] | None = None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv or argv[0] not in ("pfsp", "nqueens"):
         sys.stderr.write(__doc__ or "")
         return 2
+    if _spawn_planned(argv):
+        # the rank processes come from a forkserver that must exist before this process
+        # makes any HIP call (gpu_count, engines): a GPU-initialised process never forks
+        # and execs a rank (ref launch: pfsp_dist_multigpu_cuda.c:907-919, one MPI rank per GPU)
+        from .parallel.launch import warm_forkserver
+
+        warm_forkserver()
     return pfsp_main(argv[1:]) if argv[0] == "pfsp" else nqueens_main(argv[1:])

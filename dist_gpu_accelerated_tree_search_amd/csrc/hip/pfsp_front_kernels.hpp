@@ -93,9 +93,17 @@ struct PfspFrontArgs {
 };
 
 // Timing probe stamp k of this workgroup (thread 0; a.dbg_blk is null in production).
+// Stamp 0 also records where the workgroup runs (raw HW_ID: wave / SIMD / CU / SE fields,
+// and the XCC id) in words 12 / 13; front_local puts its node counts in word 14.
 template <class A>
 __device__ inline void front_stamp(const A& a, int k) {
-  if (a.dbg_blk && threadIdx.x == 0) a.dbg_blk[blockIdx.x * 16 + k] = wall_clock64();
+  if (a.dbg_blk && threadIdx.x == 0) {
+    a.dbg_blk[blockIdx.x * 16 + k] = wall_clock64();
+    if (k == 0) {
+      a.dbg_blk[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      a.dbg_blk[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+  }
 }
 
 template <int M>
@@ -752,6 +760,9 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
     if (tid == 0) {
       cnt_out[ch] = top;
       lcnt_out[ch] = leaves | ((pushed - top) << 16);
+      if (a.dbg_blk && ch == static_cast<int>(blockIdx.x))
+        a.dbg_blk[blockIdx.x * 16 + 14] = static_cast<unsigned long long>(pushed - top) |
+                                          (static_cast<unsigned long long>(top) << 32);
     }
   }
 }

@@ -1,0 +1,44 @@
+"""Launch hygiene of the multi-process CLI: the forkserver that
+spawns one process per GPU must start before the CLI makes any HIP call (gpu_count,
+engines), so no rank is ever fork+exec'ed from a GPU-initialised process
+(ref launch: pfsp_dist_multigpu_cuda.c:907-919, one MPI rank per GPU)."""
+import pytest
+
+from dist_gpu_accelerated_tree_search_amd import cli, ops
+from dist_gpu_accelerated_tree_search_amd.parallel import launch
+
+
+@pytest.mark.parametrize("argv,want", [
+    (["pfsp", "-D", "2", "-C", "0"], True),
+    (["pfsp", "-D", "2"], False),                      # -C 1: one process drives every GPU
+    (["pfsp", "-D", "4", "-C", "0", "--single-process"], False),
+    (["pfsp", "-D", "2", "-C", "0", "--gpus-list", "0,1"], False),
+    (["pfsp", "-D", "1", "-C", "0"], False),
+    (["pfsp", "--D=3", "--C=0"], True),
+    (["nqueens", "-N", "12", "-D", "2"], True),
+    (["nqueens", "-N", "12"], False),
+])
+def test_spawn_planned(argv, want, monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert cli._spawn_planned(argv) is want
+
+
+def test_spawn_planned_under_torchrun(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert cli._spawn_planned(["pfsp", "-D", "2", "-C", "0"]) is False
+
+
+def test_forkserver_starts_before_any_gpu_call(monkeypatch, capsys):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    calls = []
+    monkeypatch.setattr(launch, "warm_forkserver", lambda: calls.append("forkserver"))
+
+    def fake_count():
+        calls.append("gpu_count")
+        return 0  # no device: the CLI stops with the reference's message
+
+    monkeypatch.setattr(ops, "gpu_count", fake_count)
+    rc = cli.main(["pfsp", "-i", "14", "-D", "2", "-C", "0", "--no-csv"])
+    assert rc == 1
+    assert "More GPU devices requested" in capsys.readouterr().out
+    assert calls == ["forkserver", "gpu_count"], calls

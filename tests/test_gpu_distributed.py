@@ -146,3 +146,23 @@ def test_gpu_cpu_worker_per_rank():
     for r in res:
         assert (r["tree"], r["sol"], r["best"]) == (2573652, 2648, 1377)
     assert len(res[0]["workers"]) == 4
+
+
+def test_gpu_cli_spawn_two_ranks_one_device(tmp_path):
+    # the CLI's own -D 2 -C 0 path: forkserver first (cli.main), then two spawned rank
+    # processes, both on device 0, node transfers over gloo
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "-m", "dist_gpu_accelerated_tree_search_amd", "pfsp", "-i", "14", "-l", "1",
+                        "-D", "2", "-C", "0", "--comm", "gloo", "--device", "0", "--ring-gb", "0.25",
+                        "--csv-dir", str(tmp_path)],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "Size of the explored tree: 2573652" in p.stdout, p.stdout
+    assert "Optimal makespan: 1377" in p.stdout
+    assert (tmp_path / "dist_multigpu.csv").exists()
