@@ -25,8 +25,9 @@ namespace {
 using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 
 EngineConfig make_cfg(int device, size_t max_parents, size_t ring_bytes, int iters_small, int iters_large,
-                      bool use_graphs, uintptr_t stream, int iters_first) {
+                      bool use_graphs, uintptr_t stream, int iters_first, int dyn_us = 0) {
   EngineConfig c;
+  c.dyn_us = dyn_us;
   c.device = device;
   c.max_parents = max_parents;
   c.ring_bytes = ring_bytes;
@@ -175,17 +176,18 @@ PYBIND11_MODULE(_tts_hip, m) {
   m.def(
       "make_pfsp_engine",
       [](int jobs, int machines, std::vector<int> p, int lb, int device, size_t max_parents, size_t ring_bytes,
-         int iters_small, int iters_large, bool use_graphs, uintptr_t stream, int taillard_id, int iters_first) {
+         int iters_small, int iters_large, bool use_graphs, uintptr_t stream, int taillard_id, int iters_first,
+         int dyn_us) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p), taillard_id);
         py::gil_scoped_release nogil;
         return make_pfsp_engine(in, lb,
                                 make_cfg(device, max_parents, ring_bytes, iters_small, iters_large, use_graphs, stream,
-                                         iters_first));
+                                         iters_first, dyn_us));
       },
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("device") = 0,
       py::arg("max_parents") = size_t(1) << 18, py::arg("ring_bytes") = size_t(16) << 30, py::arg("iters_small") = 6,
       py::arg("iters_large") = 48, py::arg("use_graphs") = true, py::arg("stream") = 0, py::arg("taillard_id") = 0,
-      py::arg("iters_first") = 18);
+      py::arg("iters_first") = 18, py::arg("dyn_us") = 0);
 
   m.def(
       "make_queens_engine",
@@ -277,9 +279,10 @@ PYBIND11_MODULE(_tts_hip, m) {
       "pfsp_front_probe",
       [](int jobs, int machines, std::vector<int> p, int lb, U8 nodes, int best, int device, size_t max_parents,
          int fuse_max, int deep_levels, int deep_per3, int deep_per4, int local_steps, unsigned cap, int split_rank,
-         int split_world, size_t split_min, int wide_levels, int local_min) {
+         int split_world, size_t split_min, int wide_levels, int local_min, int dyn_us) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p));
         EngineConfig c;
+        c.dyn_us = dyn_us;
         c.local_min = local_min;
         c.device = device;
         c.max_parents = max_parents;
@@ -300,8 +303,8 @@ PYBIND11_MODULE(_tts_hip, m) {
         d["records"] = r.records;
         d["checked"] = r.checked;
         py::dict k;
-        const char* names[5] = {"one_level", "child_parallel", "thread_per_node", "local_dfs", "split"};
-        for (int i = 0; i < 5; ++i) k[names[i]] = r.by_kind[i];
+        const char* names[6] = {"one_level", "child_parallel", "thread_per_node", "local_dfs", "split", "dynamic"};
+        for (int i = 0; i < 6; ++i) k[names[i]] = r.by_kind[i];
         d["by_kind"] = k;
         d["bad_lb"] = r.bad_lb;
         d["bad_remain"] = r.bad_remain;
@@ -317,16 +320,17 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 16, py::arg("fuse_max") = 1 << 30,
       py::arg("deep_levels") = 2, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("local_steps") = 4,
       py::arg("cap") = 1u << 22, py::arg("split_rank") = 0, py::arg("split_world") = 1, py::arg("split_min") = 0,
-      py::arg("wide_levels") = 1, py::arg("local_min") = -1,
+      py::arg("wide_levels") = 1, py::arg("local_min") = -1, py::arg("dyn_us") = 0,
       "A complete front-kernel engine solve from these (front-layout) nodes with probe records on: every child "
       "bound of every iteration shape checked against the host oracle (counts of records and mismatches).");
   m.def(
       "pfsp_front_time",
       [](int jobs, int machines, std::vector<int> p, int lb, U8 nodes, int best, int device, size_t max_parents,
          int fuse_max, int deep_levels, int deep_per3, int deep_per4, int reps, int wide_levels, int local_min,
-         int local_steps) {
+         int local_steps, int dyn_us) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p));
         EngineConfig c;
+        c.dyn_us = dyn_us;
         c.device = device;
         c.local_min = local_min;
         c.local_steps = local_steps;
@@ -355,7 +359,7 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("nodes"), py::arg("best"),
       py::arg("device") = 0, py::arg("max_parents") = size_t(1) << 19, py::arg("fuse_max") = 1 << 30,
       py::arg("deep_levels") = 2, py::arg("deep_per3") = 8, py::arg("deep_per4") = 2, py::arg("reps") = 20,
-      py::arg("wide_levels") = 1, py::arg("local_min") = 0, py::arg("local_steps") = 4,
+      py::arg("wide_levels") = 1, py::arg("local_min") = 0, py::arg("local_steps") = 4, py::arg("dyn_us") = 0,
       "Time one front-kernel iteration over this window: min / median ms, and the per-workgroup phase stamps.");
   m.def(
       "queens_labels",

@@ -37,6 +37,9 @@ struct EngineConfig {
   int deep_levels = 2;                   // fused iterations: at most this many tree levels (kernels that have them)
   int deep_per3 = 8;                     // ... 3 levels when a workgroup takes at most this many parents
   int deep_per4 = 2;                     // ... 4 levels when a workgroup takes at most this many parents
+  // dynamic local DFS iterations (front kernel): time budget of one iteration in us
+  // (0: fixed-step local iterations)
+  int dyn_us = 0;
   int wide_levels = 1;                   // wide windows (<= one parent per thread): levels per iteration (< 2: off)
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero

@@ -27,6 +27,7 @@
 #include <deque>
 #include <memory>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../core/engine_api.hpp"
@@ -35,6 +36,12 @@
 #include "pool_device.hpp"
 
 namespace tts {
+
+// Traits with dynamic local DFS iterations (pool_device.hpp DynCtl) set kDyn = true.
+template <class T, class = void>
+struct traits_dyn : std::false_type {};
+template <class T>
+struct traits_dyn<T, std::void_t<decltype(T::kDyn)>> : std::bool_constant<T::kDyn> {};
 
 // Traits contract:
 //   using Node; using Args (with a `PoolArgs<Node> pool` member);
@@ -154,6 +161,36 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (const char* f = std::getenv("TTS_LOCAL_WIDE_STEPS")) pa.local_wide_steps = std::atoi(f);
     pa.local_narrow_steps = 6;
     if (const char* f = std::getenv("TTS_LOCAL_NARROW_STEPS")) pa.local_narrow_steps = std::atoi(f);
+    // dynamic local DFS iterations (kernels that have them, Traits::kDyn): 3 control
+    // sets, a time budget per iteration (cfg dyn_us, TTS_DYN_US; 0 = fixed-step local
+    // iterations) and the queue slots left after one chunk per resident workgroup
+    pa.dyn = nullptr;
+    pa.dyn_ticks = 0;
+    pa.dyn_q = 0;
+    if constexpr (traits_dyn<Traits>::value) {
+      int us = cfg_.dyn_us;
+      if (const char* f = std::getenv("TTS_DYN_US")) us = std::max(0, std::atoi(f));
+      const int q = static_cast<int>(std::min<size_t>(dev::kDynQMax, max_chunks_ - std::min(max_chunks_, resident))) / 8 * 8;
+      if (us > 0 && q >= 8) {
+        int rate_khz = 0;
+        TTS_HIP_CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, cfg_.device));
+        TTS_HIP_CHECK(hipMalloc(&pa.dyn, 3 * sizeof(dev::DynCtl)));
+        TTS_HIP_CHECK(hipMemset(pa.dyn, 0, 3 * sizeof(dev::DynCtl)));
+        owned_.push_back(pa.dyn);
+        pa.dyn_ticks = static_cast<int>(std::min<long long>(1ll << 30, static_cast<long long>(us) * std::max(1, rate_khz) / 1000));
+        pa.dyn_q = q;
+        if (const char* f = std::getenv("TTS_DYN_Q")) pa.dyn_q = std::max(8, std::min(q, std::atoi(f) / 8 * 8));
+      }
+    }
+    // iteration log (probes): TTS_ILOG=<file> records every iteration's window and shape
+    // (pool_device.hpp ilog_record), appended to the file when the engine is released
+    pa.ilog = nullptr;
+    if (const char* f = std::getenv("TTS_ILOG")) {
+      ilog_path_ = f;
+      TTS_HIP_CHECK(hipMalloc(&pa.ilog, kIlogWords * sizeof(dev::u64)));
+      TTS_HIP_CHECK(hipMemset(pa.ilog, 0, kIlogWords * sizeof(dev::u64)));
+      owned_.push_back(pa.ilog);
+    }
     upload_ctl();
     // Pipelined replays: queue the next graph while one runs when the last known
     // pool spans a whole parent window (spec_min_). Queuing it earlier
@@ -196,6 +233,15 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (xfer_) (void)hipStreamSynchronize(xfer_);
     trace_clear();
+    if (!ilog_path_.empty() && args_.pool.ilog) {
+      std::vector<dev::u64> log(kIlogWords);
+      if (hipMemcpy(log.data(), args_.pool.ilog, kIlogWords * sizeof(dev::u64), hipMemcpyDeviceToHost) == hipSuccess)
+        if (FILE* fp = std::fopen(ilog_path_.c_str(), "ab")) {
+          const dev::u64 n = std::min<dev::u64>(log[0], 4095);
+          std::fwrite(log.data() + 8, sizeof(dev::u64), 8 * n, fp);
+          std::fclose(fp);
+        }
+    }
     spill_.free_all();
     for (auto& gp : graphs_)
       for (auto& gs : gp)
@@ -1229,6 +1275,8 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   bool learn_first_ = true;  // first replay after begin() = the previous solve's iterations (TTS_LEARN_FIRST=0: off)
   int learned_k_ = 0;     // ... rounded up to 3k (0: unknown)
   std::vector<void*> owned_;
+  static constexpr size_t kIlogWords = 8 + 8 * 4095;
+  std::string ilog_path_;
   PinnedSpill<Node> spill_;
   EngineStats stats_;
 };

@@ -70,6 +70,7 @@ struct PfspFrontTraits {
   // backlog anyway; 4K-parent windows were slower again: profiles/r4/local_min.txt)
   static constexpr int kLocalMin = 16384;
   static constexpr int kMaxChunks = G::MAXCHUNKS;
+  static constexpr bool kDyn = true;  // dynamic local DFS iterations (front_dyn)
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
   }
@@ -480,7 +481,7 @@ std::unique_ptr<IEngine> make_pfsp_front_engine_t(const PfspInstance& in, const 
 // all records is returned too.
 struct FrontProbeResult {
   unsigned long long records = 0, checked = 0;
-  unsigned long long by_kind[5] = {};
+  unsigned long long by_kind[6] = {};
   unsigned long long bad_lb = 0, bad_remain = 0, bad_job = 0;
   EngineStats st;
   std::vector<uint32_t> first_bad;
@@ -523,7 +524,7 @@ FrontProbeResult pfsp_front_probe_t(const PfspInstance& in, int lb, const void* 
   for (size_t i = 0; i < keep; ++i) {
     const uint32_t* r = &rec[i * G::DBGW];
     const int j = static_cast<int>(r[0] & 0xffu), kind = static_cast<int>((r[0] >> 8) & 0xffu);
-    if (kind < 5) ++res.by_kind[kind];
+    if (kind < 6) ++res.by_kind[kind];
     Node parent;
     std::memcpy(&parent, r + 2, sizeof(Node));
     bool bad = false;
@@ -611,9 +612,21 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(g));  // as DeviceEngine
   TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device));
   const int grid = static_cast<int>(std::min<size_t>(max_chunks, static_cast<size_t>(std::max(1, bpc)) * cus));
+  // dynamic local DFS (as DeviceEngine): 3 control sets, the budget in wall-clock ticks
+  int dyn_us = cfg.dyn_us;
+  if (const char* f = std::getenv("TTS_DYN_US")) dyn_us = std::max(0, std::atoi(f));
+  const int dq = static_cast<int>(std::min<size_t>(dev::kDynQMax, max_chunks - std::min<size_t>(max_chunks, grid))) / 8 * 8;
+  if (dyn_us > 0 && dq >= 8) {
+    int rk = 0;
+    TTS_HIP_CHECK(hipDeviceGetAttribute(&rk, hipDeviceAttributeWallClockRate, cfg.device));
+    pa.dyn = static_cast<dev::DynCtl*>(dalloc(3 * sizeof(dev::DynCtl)));
+    pa.dyn_ticks = static_cast<int>(static_cast<long long>(dyn_us) * std::max(1, rk) / 1000);
+    pa.dyn_q = dq;
+  }
   auto restore = [&] {
     TTS_HIP_CHECK(hipMemcpy(pa.ring, nodes, n * sizeof(Node), hipMemcpyHostToDevice));
     TTS_HIP_CHECK(hipMemcpy(pa.ctl, &h, sizeof(h), hipMemcpyHostToDevice));
+    if (pa.dyn) TTS_HIP_CHECK(hipMemset(pa.dyn, 0, 3 * sizeof(dev::DynCtl)));
   };
   hipEvent_t e0, e1;
   TTS_HIP_CHECK(hipEventCreate(&e0));

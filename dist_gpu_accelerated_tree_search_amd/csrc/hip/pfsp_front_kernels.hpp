@@ -111,6 +111,13 @@ struct FrontSmem {
   using G = FrontGeom<M>;
   uint16_t ptab[G::NJ][G::MS];
   int scan[kBlock / kWave];
+  // dynamic local DFS (front_dyn): the workgroup's protocol state, in LDS so the step's
+  // registers stay those of front_local (kept in registers it spilled to scratch)
+  struct {
+    unsigned long long deadline;
+    long long inner;  // nodes pushed in this iteration and expanded here
+    int flags, dslot, best, claim, claim_n, idle, sweep, pad;
+  } dyn;
   // multi-level chunks: two levels of nodes (ping-pong), each node with its remain
   // (unscheduled work per machine, packed u16 pairs), and the child offsets of the
   // level being expanded
@@ -171,7 +178,7 @@ __device__ inline void front_store(uint4* dst, const uint32_t (&c)[FrontGeom<M>:
 // Probe record of one evaluated child (tests; a.dbg_rec is null in production): the
 // parent's words, its remain (packed u16 pairs, tails excluded), the job, the iteration
 // shape (kind) and the bound. The host recomputes every field (pfsp_front_probe).
-enum FrontDbgKind { kDbgOne = 0, kDbgCp = 1, kDbgTp = 2, kDbgLocal = 3, kDbgSplit = 4 };
+enum FrontDbgKind { kDbgOne = 0, kDbgCp = 1, kDbgTp = 2, kDbgLocal = 3, kDbgSplit = 4, kDbgDyn = 5 };
 template <int M>
 __device__ inline void front_dbg(const PfspFrontArgs<M>& a, int kind, const uint32_t (&w)[FrontGeom<M>::NW],
                                  const uint32_t (&rp)[FrontGeom<M>::HW], int j, int lb) {
@@ -767,6 +774,322 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
   }
 }
 
+// ---- dynamic local DFS (v.dyn): work moves between the workgroups of one XCD ----
+//
+// front_local with no step count: every workgroup keeps expanding the top of its own
+// stack until the iteration's time budget (pa.dyn_ticks of the 100 MHz wall clock) is
+// spent, publishing one pop (<= kBlock nodes) into a free queue slot of its XCD's
+// partition when partition workgroups wait for more blocks than are full (or when its
+// stack nears the slot region's end), and claiming a full slot when its stack runs dry
+// (ref steal-half between GPU threads, pfsp_multigpu_cuda.c:343-431, here between the
+// workgroups of one kernel). Why: per-workgroup exits of a fixed-step local iteration
+// follow the dispatch order inside each CU (corr 0.95, per-CU max exits within 10 %:
+// profiles/r5/lb_probe.txt), so the loss is not one slow workgroup but the ~10 us every
+// dependent kernel costs and the half-empty first steps of each new window
+// (profiles/r5/ilog_ta014.txt: 9 kernels, four of them local). One dynamic iteration
+// carries the tree until the budget ends or no partition workgroup has work.
+//
+// Every word and payload byte that crosses workgroups is an 8-B agent-scope atomic
+// access (sc1: L1 bypassed) on lines of the partition's own L2 — the partition is the
+// XCC id read from the hardware, never a dispatch-order assumption. Counts go to the
+// xacc lines (64-bit); the last workgroup out writes the queue chunks' counts.
+__device__ inline int dyn_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline unsigned dyn_ldu(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void dyn_stu(unsigned* p, unsigned x) {
+  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline int dyn_add(int* p, int x) {
+  return __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline bool dyn_cas(unsigned* p, unsigned expect, unsigned want) {
+  return __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int M>
+__device__ inline void dyn_node_store(PfspFrontNode<M>* dst, const uint32_t (&w)[FrontGeom<M>::NW]) {
+  u64* d = reinterpret_cast<u64*>(dst);
+#pragma unroll
+  for (int k = 0; k < FrontGeom<M>::NW / 2; ++k)
+    __hip_atomic_store(d + k, static_cast<u64>(w[2 * k]) | (static_cast<u64>(w[2 * k + 1]) << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int M>
+__device__ inline void dyn_node_load(PfspFrontNode<M>* src, uint32_t (&w)[FrontGeom<M>::NW]) {
+  u64* s = reinterpret_cast<u64*>(src);
+#pragma unroll
+  for (int k = 0; k < FrontGeom<M>::NW / 2; ++k) {
+    const u64 x = __hip_atomic_load(s + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w[2 * k] = static_cast<uint32_t>(x);
+    w[2 * k + 1] = static_cast<uint32_t>(x >> 32);
+  }
+}
+
+// Wave 0: find a slot of the partition in state `want` (0 free / 2 full, low 2 bits)
+// and move it to `to` (1 writing / 3 reading, keeping the count bits). Lanes scan 64
+// states at a time; the pick rotates with the workgroup so claimers spread. Returns
+// slot | n << 16, or -1.
+__device__ inline int dyn_take(DynCtl* dc, int qbase, int qx, unsigned want, unsigned to) {
+  const int lane = static_cast<int>(threadIdx.x) & (kWave - 1);
+  const int r = static_cast<int>(blockIdx.x) & (kWave - 1);
+  for (int k0 = 0; k0 < qx; k0 += kWave) {
+    const bool in = k0 + lane < qx;
+    const unsigned sv = in ? dyn_ldu(&dc->st[qbase + k0 + lane]) : 1u;
+    u64 hit = __ballot(in && (sv & 3u) == want);
+    while (hit) {
+      const u64 rot = r ? ((hit >> r) | (hit << (kWave - r))) : hit;
+      const int pick = (__builtin_ctzll(rot) + r) & (kWave - 1);
+      bool ok = false;
+      if (lane == pick) ok = dyn_cas(&dc->st[qbase + k0 + pick], sv, (sv & ~3u) | to);
+      ok = __shfl(static_cast<int>(ok), pick, kWave) != 0;
+      const unsigned n = static_cast<unsigned>(__shfl(static_cast<int>(sv), pick, kWave)) >> 8;
+      if (ok) return (k0 + pick) | static_cast<int>(n << 16);
+      hit &= ~(1ull << pick);
+    }
+  }
+  return -1;
+}
+
+template <int M>
+__device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t, int best0) {
+  using G = FrontGeom<M>;
+  using Node = PfspFrontNode<M>;
+  constexpr int NW = G::NW;
+  const int tid = threadIdx.x;
+  const auto& pa = a.pool;
+  const int ch = static_cast<int>(blockIdx.x);  // v.nchunks == gridDim.x: chunk ch is workgroup ch's stack
+  Node* const stk = pa.buf[(t & 1) ^ 1] + static_cast<size_t>(ch) * G::SLOT;
+  // partition state (wave 0 only): the XCD's queue slots and counters
+  auto qslot = [&](int q) {
+    const int xcc = static_cast<int>(__builtin_amdgcn_s_getreg((31 << 11) | 20)) & 7;  // HW_REG_XCC_ID
+    return xcc * (v.qn / 8) + q;
+  };
+  auto part = [&]() -> DynCtl::Part& {
+    return pa.dyn[t % 3].part[static_cast<int>(__builtin_amdgcn_s_getreg((31 << 11) | 20)) & 7];
+  };
+  // slot q of the partition: the output chunk region nchunks + the slot's queue index
+  auto region = [&](int q) { return pa.buf[(t & 1) ^ 1] + static_cast<size_t>(v.nchunks + qslot(q)) * G::SLOT; };
+  if (tid == 0) {
+    sm.dyn.deadline = wall_clock64() + static_cast<u64>(pa.dyn_ticks);  // the budget runs from this start
+    sm.dyn.inner = 0;
+    sm.dyn.claim = -1;
+    sm.dyn.idle = 0;
+    dyn_add(&part().busy, 1);
+  }
+  int top = 0, nst = 0, best = best0, nleaf = 0;
+  for (int s = 0;; ++s) {
+    uint32_t w[NW], rp[G::HW];
+    bool have_r = false;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w[i] = 0;
+    const int claim = s == 0 ? -1 : sm.dyn.claim;
+    if (s == 0) {
+      const u64 gi = static_cast<u64>(ch) + static_cast<u64>(tid) * static_cast<u64>(v.nchunks);
+      if (tid < v.bp && gi < v.B) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
+    } else if (claim >= 0) {
+      if (tid < sm.dyn.claim_n) dyn_node_load<M>(region(claim) + tid, w);
+    } else {
+      const int npop = min(top, kBlock);
+      if (tid < npop) {
+        const int k = tid - (npop - nst);
+        if (k >= 0) {
+#pragma unroll
+          for (int q = 0; q < G::VPN; ++q) {
+            const uint4 x = sm.stage[k][q];
+            w[4 * q] = x.x;
+            w[4 * q + 1] = x.y;
+            w[4 * q + 2] = x.z;
+            w[4 * q + 3] = x.w;
+          }
+#pragma unroll
+          for (int h = 0; h < G::HW; ++h) rp[h] = sm.stage_r[k][h];
+          have_r = true;
+        } else {
+          front_load<M>(stk + (top - npop + tid), w);
+        }
+      }
+      top -= npop;
+      if (tid == 0) sm.dyn.inner += npop;
+    }
+    uint32_t surv = 0;
+    int nsurv = 0;
+    const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
+    if (!have_r) front_remain<M>(sm, w, rp);
+    front_parent_r<M>(
+        a, sm, w, rp,
+        [&](int j, int lb) {
+          if (leaf) {
+            ++nleaf;
+            if (lb < best) atomicMin(&pa.ctl->best.v, lb);
+          } else if (lb < best) {
+            ++nsurv;
+            surv |= 1u << j;
+          }
+        },
+        kDbgDyn);
+    int tot = 0;
+    const int off = block_exclusive_scan(nsurv, sm.scan, &tot);
+    // (the scan's barrier: every thread holds its node in registers; a claimed slot is read)
+    const int tnew = top + tot;
+    nst = min(tot, min(tnew, kBlock));  // the next pop stays in LDS
+    const int lo = tot - nst;
+    uint4* const dst = reinterpret_cast<uint4*>(stk + top);
+    front_emit_to<M>(sm, w, surv, [&](int i, const uint32_t (&c)[NW], int j) {
+      const int o = off + i;
+      if (o >= lo) {
+        front_store<M>(&sm.stage[o - lo][0], c);
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
+#pragma unroll
+        for (int h = 0; h < G::HW; ++h) sm.stage_r[o - lo][h] = rp[h] - row[h];
+      } else {
+        front_store<M>(dst + o * G::VPN, c);
+      }
+    });
+    top = tnew;
+    // wave 0 decides what follows: free a claimed slot, stop at the deadline, publish the
+    // next pop when partition workgroups wait for more blocks than are full (or when the
+    // stack nears the end of its region)
+    if (tid < kWave) {
+      int flags = 0, dslot = -1;
+      if (tid == 0) {
+        if (claim >= 0) {
+          sm.dyn.inner += sm.dyn.claim_n;
+          dyn_stu(&pa.dyn[t % 3].st[qslot(claim)], 0u);
+        }
+        if (wall_clock64() >= sm.dyn.deadline) flags = 1;
+      }
+      flags = __shfl(flags, 0, kWave);
+      if (!flags && top >= 2 * kBlock) {
+        int want = 0;
+        if (tid == 0)
+          want = top + kBlock * (G::NJ - 1) > G::SLOT || dyn_ld(&part().hungry) > dyn_ld(&part().avail);
+        if (__shfl(want, 0, kWave)) {
+          const int r = dyn_take(pa.dyn + t % 3, qslot(0), v.qn / 8, 0u, 1u);
+          dslot = r < 0 ? -1 : (r & 0xffff);
+        }
+      }
+      if (tid == 0) {
+        sm.dyn.flags = flags;
+        sm.dyn.dslot = dslot;
+        sm.dyn.claim = -1;
+        sm.dyn.best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();  // pushes visible to the next pops; decisions in sm.dyn
+    if (s < 4) front_stamp(a, 4 + s);
+    best = min(best, sm.dyn.best);
+    if (sm.dyn.dslot >= 0) {
+      const int n = min(top, kBlock);
+      if (tid < n) {
+        uint32_t x[NW];
+        const int k = tid - (n - nst);
+        if (k >= 0) {
+#pragma unroll
+          for (int q = 0; q < G::VPN; ++q) {
+            const uint4 y = sm.stage[k][q];
+            x[4 * q] = y.x;
+            x[4 * q + 1] = y.y;
+            x[4 * q + 2] = y.z;
+            x[4 * q + 3] = y.w;
+          }
+        } else {
+          front_load<M>(stk + (top - n + tid), x);
+        }
+        dyn_node_store<M>(region(sm.dyn.dslot) + tid, x);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload is complete
+      __syncthreads();
+      if (tid == 0) {
+        dyn_stu(&pa.dyn[t % 3].st[qslot(sm.dyn.dslot)], 2u | (static_cast<unsigned>(n) << 8));
+        dyn_add(&part().avail, 1);
+      }
+      top -= n;
+      nst = 0;
+    }
+    if (sm.dyn.flags) break;
+    if (top + kBlock * (G::NJ - 1) > G::SLOT) break;  // a full pop could overflow the region
+    if (top == 0) {
+      // stack dry: claim a published block of the partition (wave 0; the others wait)
+      if (tid < kWave) {
+        if (tid == 0 && !sm.dyn.idle) {
+          dyn_add(&part().busy, -1);
+          dyn_add(&part().hungry, 1);
+          sm.dyn.idle = 1;
+        }
+        int r = -1;
+        for (int spin = 0; spin < (1 << 20); ++spin) {
+          r = dyn_take(pa.dyn + t % 3, qslot(0), v.qn / 8, 2u, 3u);
+          if (r >= 0) break;
+          int stop = 0;
+          if (tid == 0)
+            stop = wall_clock64() >= sm.dyn.deadline || (dyn_ld(&part().busy) == 0 && dyn_ld(&part().avail) == 0);
+          if (__shfl(stop, 0, kWave)) break;
+          __builtin_amdgcn_s_sleep(16);
+        }
+        if (tid == 0 && r >= 0) {
+          dyn_add(&part().busy, 1);
+          dyn_add(&part().hungry, -1);
+          dyn_add(&part().avail, -1);
+          sm.dyn.idle = 0;
+          sm.dyn.claim = r & 0xffff;
+          sm.dyn.claim_n = r >> 16;
+        }
+      }
+      __syncthreads();
+      if (sm.dyn.claim < 0) break;
+    }
+  }
+  // the nodes staged for a next step are the top of the stack
+  if (tid < nst) {
+    uint32_t x[NW];
+#pragma unroll
+    for (int q = 0; q < G::VPN; ++q) {
+      const uint4 y = sm.stage[tid][q];
+      x[4 * q] = y.x;
+      x[4 * q + 1] = y.y;
+      x[4 * q + 2] = y.z;
+      x[4 * q + 3] = y.w;
+    }
+    front_store<M>(reinterpret_cast<uint4*>(stk + (top - nst + tid)), x);
+  }
+  int leaves = 0;
+  (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
+  int* const cnt_out = pa.cnt[(t & 1) ^ 1];
+  int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
+  if (tid == 0) {
+    dyn_add(sm.dyn.idle ? &part().hungry : &part().busy, -1);
+    cnt_out[ch] = top;
+    lcnt_out[ch] = 0;
+    auto& x = pa.ctl->xacc[ch & 7];
+    const long long inner = sm.dyn.inner;
+    if (inner) __hip_atomic_fetch_add(&x.tree, static_cast<u64>(inner), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (leaves) __hip_atomic_fetch_add(&x.sol, static_cast<u64>(leaves), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.dbg_blk)
+      a.dbg_blk[blockIdx.x * 16 + 14] = static_cast<unsigned long long>(inner) |
+                                        (static_cast<unsigned long long>(top) << 32);
+    // the last workgroup out (every slot state final) writes the queue chunks' counts
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DynCtl* const dc = pa.dyn + t % 3;
+    const int g = ch & 7;
+    const int gs = (static_cast<int>(gridDim.x) - g + 7) / 8;
+    int sweep = 0;
+    if (dyn_add(&dc->fin[g].n, 1) == gs - 1)
+      sweep = dyn_add(&dc->fin[8].n, 1) == min(8, static_cast<int>(gridDim.x)) - 1;
+    sm.dyn.sweep = sweep;
+  }
+  __syncthreads();
+  if (sm.dyn.sweep) {
+    DynCtl* const dc = pa.dyn + t % 3;
+    for (int q = tid; q < v.qn; q += kBlock) {
+      const unsigned sv = dyn_ldu(&dc->st[q]);
+      cnt_out[v.nchunks + q] = (sv & 3u) == 2u ? static_cast<int>(sv >> 8) : 0;
+      lcnt_out[v.nchunks + q] = 0;
+    }
+  }
+}
+
 // One B&B iteration on the device-resident pool (pool_device.hpp); t in [0, 6): state
 // slot t % 3, buffer parity t % 2.
 //
@@ -792,7 +1115,8 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     const int x = tid + i * kBlock;
     ptv[i] = x < a.jobs * G::MS ? a.ptab[x] : 0;
   }
-  const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, a.bpf, G::LT, G::NJ * (G::NJ - 1), G::LMAX);
+  const IterView v =
+      pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool, a.bpf, G::LT, G::NJ * (G::NJ - 1), G::LMAX, true);
   front_stamp(a, 1);
   if (v.B == 0 || v.overflow) return;
   {
@@ -808,6 +1132,11 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
   pool_spill_leftovers<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, sm.pool);
   __syncthreads();
   front_stamp(a, 2);
+  if (v.dyn) {
+    front_dyn<M>(a, sm, v, t, best);
+    front_stamp(a, 15);
+    return;
+  }
   if (v.local) {
     front_local<M>(a, sm, v, t, best);
     front_stamp(a, 15);

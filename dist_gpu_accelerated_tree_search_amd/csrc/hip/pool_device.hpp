@@ -67,6 +67,32 @@ struct PoolCtl {
   CtlI32 best;      // incumbent (atomicMin by leaves)
 };
 
+// Dynamic local DFS iterations (kernels that implement them, front_dyn): one iteration's
+// control, in 3 rotating sets — iteration t uses set t % 3 and zeroes set (t + 1) % 3 for
+// the next one (the slot rotation of PoolCtl; kernels of one stream never overlap).
+// Work moves between the workgroups of ONE XCD (partition = the XCC id read from the
+// hardware, so the L2 every hand-off goes through is shared by construction): a workgroup
+// whose stack holds more than it needs publishes one pop (<= kBlock nodes) into a free
+// slot of its partition; a workgroup whose stack ran dry claims a full slot. Slots are
+// chunk regions past the workgroups' own ([grid, grid + qn) of the output buffer), so a
+// block nobody claimed is simply an output chunk (its count written by the last
+// workgroup to leave).
+constexpr int kDynQMax = 1024;
+struct DynCtl {
+  struct alignas(128) Part {
+    int busy;    // workgroups of the partition with work (a stack or a claimed block)
+    int hungry;  // ... waiting for a block
+    int avail;   // full slots
+    int pad[29];
+  } part[8];
+  struct alignas(128) Fin {
+    int n;
+    int pad[31];
+  } fin[9];  // workgroups gone per blockIdx % 8 group; [8]: groups gone
+  // slot state: 0 free, 1 being written, 2 | n << 8 full (n nodes), 3 | n << 8 being read
+  unsigned st[kDynQMax];
+};
+
 template <class Node>
 struct PoolArgs {
   Node* ring;
@@ -93,7 +119,34 @@ struct PoolArgs {
   // wide multi-level iterations: a window of more than a narrow chunk's parents per
   // workgroup but at most one per thread is expanded this many levels deep (< 2: off)
   int wide_levels;
+  // dynamic local DFS (front kernel): 3 DynCtl sets (null: off), the time budget of
+  // one iteration in wall-clock ticks (100 MHz) and the queue slots (a multiple of 8)
+  DynCtl* dyn;
+  int dyn_ticks;
+  int dyn_q;
+  // iteration log (probe builds: -DTTS_ILOG_BUILD, scripts/build_variant.py; env TTS_ILOG):
+  // word 0 counts records, record r
+  // at 8 + 8 r holds {wall clock at pool_begin, S, C, B, shape word, tree so far, t, 0}
+  u64* ilog;
 };
+
+// Shape word of an iteration log record: chunks | bp << 20 | steps << 36 | flags << 44
+// (bit 0 local, 1 stride, 2 fused, 3 split, 4 armed, 5 overflow; levels << 48).
+__device__ inline void ilog_record(u64* ilog, u64 clk, u64 S, u64 C, u64 B, int nchunks, int bp, int steps,
+                                   int flags, int levels, u64 tree, int t) {
+  const u64 r = ilog[0];
+  if (r >= 4095) return;
+  u64* x = ilog + 8 + 8 * r;
+  x[0] = clk;
+  x[1] = S;
+  x[2] = C;
+  x[3] = B;
+  x[4] = static_cast<u64>(nchunks) | (static_cast<u64>(bp) << 20) | (static_cast<u64>(steps & 0xff) << 36) |
+         (static_cast<u64>(flags & 0xff) << 44) | (static_cast<u64>(levels & 0xf) << 48);
+  x[5] = tree;
+  x[6] = static_cast<u64>(t);
+  ilog[0] = r + 1;
+}
 
 // Per-chunk leaf word: leaves in the low 16 bits; the high 16 bits count the
 // children a two-level iteration pushed and expanded itself (explored tree).
@@ -195,7 +248,17 @@ struct IterView {
   int cap;            // local DFS: no further step once the stack holds more than this
   int srank, sworld;
   bool armed;         // a rank split is pending: the pool is replicated on every rank
+  bool dyn;           // dynamic local DFS (front_dyn): chunk ch = workgroup ch, queue chunks after them
+  int qn;             // dynamic: queue slots (output chunks [nchunks, nchunks + qn))
 };
+
+// Zero the DynCtl set the next iteration uses (workgroup 0, every launch of a kernel that
+// has dynamic iterations; busy starts at 0 and counts workgroups in as they start).
+__device__ inline void dyn_zero_next(DynCtl* dyn, int t) {
+  if (!dyn || blockIdx.x != 0) return;
+  uint32_t* d = reinterpret_cast<uint32_t*>(dyn + (t + 1) % 3);
+  for (int i = threadIdx.x; i < static_cast<int>(sizeof(DynCtl) / 4); i += kBlock) d[i] = 0;
+}
 
 // Does this rank keep child position k of window parent gi? (always, outside the
 // split iteration). The owner is a hash of (gi, k) (splitmix64 finalizer): a plain
@@ -225,7 +288,7 @@ template <class Node, int MAXCHUNKS>
 // levels; what is left on the stack is the chunk's output. Several tree levels per
 // dependent kernel, and the next iteration re-deals the stacks over the grid.
 __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, PoolSmem<MAXCHUNKS>& ps,
-                                      int BPF = 0, int LT = 1, int GROW2 = 0, int LMAX = 2) {
+                                      int BPF = 0, int LT = 1, int GROW2 = 0, int LMAX = 2, bool DYN = false) {
   const int s_in = t % 3, s_out = (t + 1) % 3;
   const int b_in = t & 1;
   PoolCtl* ctl = pa.ctl;
@@ -246,8 +309,10 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     // and leave — no table staging, no scans, no counter traffic
     v.C = v.B = v.nb = v.ns = v.L = v.Snew = v.bot = 0;
     v.nchunks = 0;
-    v.overflow = v.split = v.fused = v.local = v.armed = v.stride = false;
+    v.overflow = v.split = v.fused = v.local = v.armed = v.stride = v.dyn = false;
+    v.qn = 0;
     v.levels = 1;
+    if (DYN) dyn_zero_next(pa.dyn, t);
     v.bp = BP;
     v.steps = v.cap = 0;
     v.srank = v.sworld = 0;
@@ -255,6 +320,9 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
       ctl->slot[s_out].stack = 0;
       ctl->slot[s_out].nch = 0;
       ctl->slot[s_out].sdone = done_in;
+#ifdef TTS_ILOG_BUILD  // (probe builds only: its live values made the front kernel spill)
+      if (pa.ilog) ilog_record(pa.ilog, wall_clock64(), 0, 0, 0, 0, 0, 0, 0, 0, ctl->tree, t);
+#endif
     }
     return v;
   }
@@ -289,6 +357,13 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   if (v.stride && pa.local_narrow_steps > 0 && v.sworld > 1 && done_in && min(v.B, full) < 64ull * gridDim.x)
     v.steps = pa.local_narrow_steps;
   v.cap = pa.local_cap > 0 ? pa.local_cap : 0x7fffffff;
+  // dynamic local DFS: every workgroup owns its chunk (the window dealt strided over the
+  // grid) and steps until the time budget, sharing work through the queue slots
+  v.dyn = DYN && v.local && pa.dyn != nullptr && pa.dyn_ticks > 0 && pa.dyn_q > 0 &&
+          static_cast<int>(gridDim.x) + pa.dyn_q <= pa.max_chunks;
+  v.qn = v.dyn ? pa.dyn_q : 0;
+  if (v.dyn) v.stride = true;
+  if (DYN) dyn_zero_next(pa.dyn, t);
   if (v.local) v.B = min(v.B, full);
   v.nb = min(v.B, v.C);
   v.ns = v.B - v.nb;
@@ -340,7 +415,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     bp = static_cast<int>(min(static_cast<u64>(BP), max(per, 1ull)));
   }
   v.bp = bp;
-  v.nchunks = static_cast<int>((v.B + bp - 1) / bp);
+  v.nchunks = v.dyn ? static_cast<int>(gridDim.x) : static_cast<int>((v.B + bp - 1) / bp);
   const bool overflow = v.overflow;
   v.overflow = overflow || bad_split;
   if (blockIdx.x == 0) {
@@ -352,7 +427,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     (void)block_exclusive_scan(in, ps.scan, &in_total);
     if (threadIdx.x == 0) {
       ctl->slot[s_out].stack = v.overflow ? v.S : v.Snew;
-      ctl->slot[s_out].nch = v.overflow ? 0 : v.nchunks;
+      ctl->slot[s_out].nch = v.overflow ? 0 : v.nchunks + v.qn;
       ctl->slot[s_out].sdone = (done_in || v.split) ? 1 : 0;
       if (v.split && v.srank != 0) {
         // everything counted so far was explored identically by every rank: rank 0 keeps it
@@ -368,6 +443,13 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
       }
       if (overflow) ctl->overflow = 1;
       else if (bad_split) ctl->overflow = 2;
+#ifdef TTS_ILOG_BUILD
+      if (pa.ilog)
+        ilog_record(pa.ilog, wall_clock64(), v.S, v.C, v.B, v.nchunks, v.bp, v.local ? v.steps : 0,
+                    (v.local ? 1 : 0) | (v.stride ? 2 : 0) | (v.fused ? 4 : 0) | (v.split ? 8 : 0) |
+                        (v.armed ? 16 : 0) | (v.overflow ? 32 : 0) | (v.dyn ? 64 : 0),
+                    v.levels, ctl->tree, t);
+#endif
     }
   }
   return v;

@@ -53,6 +53,10 @@ class EngineOptions:
     # with one engine, 0.30 / 0.39 ms split over 2 / 3 streams (a latency-bound tree
     # gains nothing from concurrent streams; profiles/r3/probes/headline_streams_split_ab.txt)
     stream_split: int = 0
+    # dynamic local DFS iterations of the LB1 / LB1_d front kernel (csrc/hip/pfsp_front_kernels.hpp
+    # front_dyn): time budget of one iteration in us, work shared between the workgroups of
+    # an XCD; 0 = fixed-step local iterations
+    dyn_us: int = 0
 
 
 def make_multi(model, backend: str, device: int, opts: EngineOptions):
@@ -151,7 +155,7 @@ class PfspModel:
                                   max_parents=opts.max_parents, ring_bytes=opts.ring_bytes,
                                   iters_small=opts.iters_small, iters_large=opts.iters_large,
                                   use_graphs=opts.use_graphs, taillard_id=self.inst_id,
-                                  iters_first=opts.iters_first)
+                                  iters_first=opts.iters_first, dyn_us=opts.dyn_us)
 
     def make_hybrid(self, engine, backend: str, threads: int, m: int = 25, cap: int = 20000, batch: int = 5000):
         """`engine` plus a CPU worker of `threads` threads as one rank engine
