@@ -225,11 +225,18 @@ inline DistOptions dist_options_from(const py::dict& o) {
   return opt;
 }
 
+// A native control plane object (HIP module: RcclTransport) in place of a Python
+// all-gather callable: returns null when `obj` is not one.
+using NativeControl = std::function<std::unique_ptr<RoundControl>(py::object obj, IEngine* e)>;
+
 inline std::unique_ptr<RoundControl> round_control_from(uintptr_t shm_address, py::object allgather_fn, int rank,
-                                                        int world, double timeout_s) {
+                                                        int world, double timeout_s, const NativeControl& native = {},
+                                                        IEngine* e = nullptr) {
   using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
   std::unique_ptr<RoundControl> ctl;
-  if (shm_address) {
+  if (!shm_address && native && !allgather_fn.is_none()) ctl = native(allgather_fn, e);
+  if (ctl) {
+  } else if (shm_address) {
     ctl = std::make_unique<ShmRoundControl>(reinterpret_cast<ShmControl*>(shm_address), timeout_s);
   } else {
     if (allgather_fn.is_none()) throw std::invalid_argument("give a shm address or an allgather_fn");
@@ -330,7 +337,8 @@ inline TransferFn resolve_transfer(const NativeTransfer& native, py::object obj,
   return transfer_from(obj);
 }
 
-inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory, NativeTransfer native = {}) {
+inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory, NativeTransfer native = {},
+                             NativeControl native_ctl = {}) {
   m.def(
       "p2p_calls",
       [](py::list plan, int rank) {
@@ -349,20 +357,25 @@ inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory, Nativ
   m.def(
       "plan_transfers",
       [](std::vector<int64_t> sizes, size_t needy_below, size_t donor_min, size_t cap, int local_world, bool intra,
-         bool inter) {
+         bool inter, std::vector<int64_t> give) {
         py::list out;
-        for (const auto& t : plan_transfers(sizes, needy_below, donor_min, cap, local_world, intra, inter))
+        const size_t n = sizes.size();
+        if (!give.empty() && give.size() != n) throw std::invalid_argument("give: one value per rank");
+        for (const auto& t : plan_transfers(sizes, std::vector<size_t>(n, needy_below), std::vector<size_t>(n, donor_min),
+                                            std::vector<size_t>(n, cap), local_world, intra, inter,
+                                            give.empty() ? nullptr : &give))
           out.append(py::make_tuple(t.donor, t.receiver, t.n));
         return out;
       },
       py::arg("sizes"), py::arg("needy_below"), py::arg("donor_min"), py::arg("cap"), py::arg("local_world") = 0,
-      py::arg("intra") = true, py::arg("inter") = true);
+      py::arg("intra") = true, py::arg("inter") = true, py::arg("give") = std::vector<int64_t>{},
+      "give: what each rank can export right now (a rank with a replay in flight); donors hand over at most that.");
   m.def(
       "dist_rounds",
-      [native](IEngine& e, uintptr_t shm_address, py::object allgather_fn, int rank, int world, py::dict o,
+      [native, native_ctl](IEngine& e, uintptr_t shm_address, py::object allgather_fn, int rank, int world, py::dict o,
          py::object transfer_fn, py::object round_hook, unsigned long long rounds0, double timeout_s) {
         const DistOptions opt = dist_options_from(o);
-        auto ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s);
+        auto ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s, native_ctl, &e);
         const TransferFn xfer = resolve_transfer(native, transfer_fn, &e);
         const RoundHook hook = hook_from(round_hook);
         DistOutcome out;
@@ -377,14 +390,14 @@ inline void bind_dist_rounds(py::module_& m, WarmupFactory warmup_factory, Nativ
       py::arg("timeout_s") = 1800.0,
       "Native lock-step rounds of a multi-rank solve until every pool is empty (or max_rounds).");
   py::class_<PyDistSession>(m, "DistSession", py::module_local())
-      .def(py::init([warmup_factory, native](py::object engine, py::object model, uintptr_t shm_address, py::object allgather_fn,
+      .def(py::init([warmup_factory, native, native_ctl](py::object engine, py::object model, uintptr_t shm_address, py::object allgather_fn,
                                      int rank, int world, py::dict o, py::object transfer_fn, py::object round_hook,
                                      size_t warm_target, size_t split_min, double timeout_s, bool split) {
              auto s = std::make_unique<PyDistSession>();
              s->split = split;
              s->engine_ref = engine;
              s->e = engine.cast<IEngine*>();
-             s->ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s);
+             s->ctl = round_control_from(shm_address, allgather_fn, rank, world, timeout_s, native_ctl, s->e);
              s->opt = dist_options_from(o);
              s->warm = warmup_factory(model);
              s->xfer = resolve_transfer(native, transfer_fn, s->e);

@@ -101,7 +101,20 @@ PYBIND11_MODULE(_tts_hip, m) {
       .def_property_readonly("device", &RcclTransport::device)
       .def_property_readonly("transfers", &RcclTransport::transfers)
       .def_property_readonly("bytes_sent", &RcclTransport::bytes_sent)
-      .def_property_readonly("bytes_recv", &RcclTransport::bytes_recv);
+      .def_property_readonly("bytes_recv", &RcclTransport::bytes_recv)
+      .def_property_readonly("collectives", &RcclTransport::collectives)
+      .def(
+          "allgather_i64",
+          [](RcclTransport& t, std::vector<int64_t> v, IEngine& e) {
+            py::array_t<int64_t> out({static_cast<py::ssize_t>(t.world()), static_cast<py::ssize_t>(v.size())});
+            {
+              py::gil_scoped_release nogil;
+              t.allgather_i64(v.data(), static_cast<int>(v.size()), out.mutable_data(), e);
+            }
+            return out;
+          },
+          py::arg("values"), py::arg("engine"),
+          "Status all-gather over the communicator on the engine's transfer stream -> (world, n) int64.");
   const NativeTransfer native_rccl = [](py::object obj, IEngine* e) -> TransferFn {
     if (!py::isinstance<RcclTransport>(obj)) return {};
     RcclTransport* t = obj.cast<RcclTransport*>();
@@ -117,7 +130,11 @@ PYBIND11_MODULE(_tts_hip, m) {
       return with_pfsp_problem(*inst, lb, [&](auto prob) -> WarmupFn { return make_warmup(inst, prob); });
     }
     return make_warmup(nullptr, QueensProblem(model.attr("N").cast<int>(), model.attr("G").cast<int>()));
-  }, native_rccl);
+  }, native_rccl, [](py::object obj, IEngine* e) -> std::unique_ptr<RoundControl> {
+    // the RCCL transport as the round loop's control plane (ncclAllGather, no Python)
+    if (!py::isinstance<RcclTransport>(obj) || !e) return nullptr;
+    return std::make_unique<RcclRoundControl>(obj.cast<RcclTransport*>(), e);
+  });
   bind_runner(
       m, []() -> std::unique_ptr<DeviceStaging> { return std::make_unique<HipStaging>(); }, &device_cpus);
   if (!std::getenv("TTS_NO_ROCTX")) install_roctx_hooks();

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <exception>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -28,7 +29,12 @@ class CpuEngine final : public IEngine {
 
   CpuEngine(Problem prob, size_t batch, int threads) : prob_(std::move(prob)), batch_(std::max<size_t>(1, batch)),
                                                         threads_(std::max(1, threads)) {}
-  ~CpuEngine() override { join_bg(); }
+  ~CpuEngine() override {
+    try {
+      join_bg();
+    } catch (...) {  // a failed background batch: nothing left to report it to
+    }
+  }
 
   size_t node_bytes() const override { return sizeof(Node); }
   size_t size() override {
@@ -154,6 +160,7 @@ class CpuEngine final : public IEngine {
   bool split_pending() override { return split_world_ > 1 && !split_done_; }
   void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
   double pool_weight(const std::vector<double>& w) override {
+    join_bg();  // the background batch may reallocate the pool
     double s = 0;
     if (w.empty()) return s;
     for (size_t i = 0; i < pool_.size(); ++i)
@@ -167,6 +174,7 @@ class CpuEngine final : public IEngine {
   }
 
   size_t warm_split(int rank, int world, size_t window, int passes) override {
+    join_bg();
     const double t0 = now_s();
     std::vector<Node> parents(std::max<size_t>(1, window));
     for (int i = 0; i < passes * 6 && !pool_.empty(); ++i) {
@@ -236,7 +244,14 @@ class CpuEngine final : public IEngine {
       int b = b0;
       u64 tr = 0, so = 0;
       std::vector<Node> kids;
-      for (const Node& p : mine) prob_.decompose(p, b, tr, so, [&](const Node& c) { kids.push_back(c); });
+      try {
+        for (const Node& p : mine) prob_.decompose(p, b, tr, so, [&](const Node& c) { kids.push_back(c); });
+      } catch (...) {  // rethrown to the caller by join_bg (never std::terminate)
+        std::lock_guard<std::mutex> lk(mu_);
+        bg_error_ = std::current_exception();
+        bg_n_ = 0;
+        return;
+      }
       std::lock_guard<std::mutex> lk(mu_);
       pool_.push_back_bulk_free(kids.data(), kids.size());
       tree_ += tr;
@@ -250,9 +265,14 @@ class CpuEngine final : public IEngine {
   void join_bg() {
     if (!bg_.joinable()) return;
     bg_.join();
-    std::lock_guard<std::mutex> lk(mu_);
-    best_ = std::min({best_, bg_best_, pending_best_});
-    bg_best_ = pending_best_ = 0x7fffffff;
+    std::exception_ptr err;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      best_ = std::min({best_, bg_best_, pending_best_});
+      bg_best_ = pending_best_ = 0x7fffffff;
+      std::swap(err, bg_error_);
+    }
+    if (err) std::rethrow_exception(err);
   }
 
   // Same contract as the device split: identical breadth-first expansion on every
@@ -318,6 +338,7 @@ class CpuEngine final : public IEngine {
   // overlapped rounds (leave_one / join_bg)
   std::mutex mu_;
   std::thread bg_;
+  std::exception_ptr bg_error_;  // an exception of the background batch (join_bg rethrows it)
   size_t bg_n_ = 0;
   int bg_best_ = 0x7fffffff, pending_best_ = 0x7fffffff;
   bool overlap_ = false;

@@ -116,12 +116,15 @@ using Plan = std::vector<Transfer>;
 // GPU thief, 4*T for a CPU one: pfsp_multigpu_cuda.c:369-372). intra/inter
 // restrict pairs to the same node (-w) or to different nodes (-L); node = rank /
 // local_world.
+// give (optional, per donor): what each rank can export without waiting (a rank with
+// work in flight: DeviceEngine::size_exportable); a donor hands over at most that.
 inline Plan plan_transfers(const std::vector<int64_t>& sizes, const std::vector<size_t>& needy_below,
                            const std::vector<size_t>& donor_min, const std::vector<size_t>& cap, int local_world = 0,
-                           bool intra = true, bool inter = true) {
+                           bool intra = true, bool inter = true, const std::vector<int64_t>* give = nullptr) {
   const int n = static_cast<int>(sizes.size());
   const int lw = local_world > 0 ? local_world : std::max(1, n);
   std::vector<int64_t> left = sizes;
+  std::vector<int64_t> avail = give ? *give : sizes;
   std::vector<char> needy(n);
   for (int r = 0; r < n; ++r) needy[r] = sizes[r] < static_cast<int64_t>(needy_below[r]);
   Plan plan;
@@ -129,15 +132,16 @@ inline Plan plan_transfers(const std::vector<int64_t>& sizes, const std::vector<
     if (!needy[r]) continue;
     int d = -1;
     for (int x = 0; x < n; ++x) {
-      if (x == r || needy[x] || left[x] < static_cast<int64_t>(donor_min[x])) continue;
+      if (x == r || needy[x] || left[x] < static_cast<int64_t>(donor_min[x]) || avail[x] <= 0) continue;
       const bool same = x / lw == r / lw;
       if (!((intra && same) || (inter && !same))) continue;
       if (d < 0 || left[x] > left[d]) d = x;
     }
     if (d < 0) continue;
-    const size_t k = std::min(static_cast<size_t>(left[d] / 2), cap[r]);
+    const size_t k = std::min({static_cast<size_t>(left[d] / 2), cap[r], static_cast<size_t>(std::max<int64_t>(0, avail[d]))});
     if (k == 0) continue;
     left[d] -= static_cast<int64_t>(k);
+    avail[d] -= static_cast<int64_t>(k);
     left[r] += static_cast<int64_t>(k);
     plan.push_back({d, r, k});
   }
@@ -326,8 +330,9 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
   } no_overlap{e, overlap};
   unsigned long long overlapped = 0;
 
-  constexpr int kRec = 4;  // status record: pool size, incumbent, split pending, time up
-  std::vector<int64_t> st(static_cast<size_t>(world) * kRec), sizes(world);
+  // status record: pool size, incumbent, split pending, time up, exportable now
+  constexpr int kRec = 5;
+  std::vector<int64_t> st(static_cast<size_t>(world) * kRec), sizes(world), gives(world);
   const auto t_begin = clock::now();
   const int lw = o.local_world > 0 ? o.local_world : std::max(1, world);
   // ranks that may donate to this one (the pair filter of plan_transfers)
@@ -348,6 +353,7 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     const bool flying = overlap && e.in_flight();
     overlapped += flying;
     const int64_t size = static_cast<int64_t>(flying ? e.size_known() : e.size());
+    const int64_t give = flying ? static_cast<int64_t>(e.size_exportable()) : size;
     const int mybest = flying ? e.best_known() : e.best();
     const bool pend = flying ? e.split_pending_known() : e.split_pending();
     ctl.publish_size(size);
@@ -369,7 +375,7 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
       ++early;
     }
     const bool timeup = o.time_limit > 0 && secs(t_begin, clock::now()) >= o.time_limit;
-    const int64_t mine[kRec] = {size, mybest, pend ? 1 : 0, timeup ? 1 : 0};
+    const int64_t mine[kRec] = {size, mybest, pend ? 1 : 0, timeup ? 1 : 0, give};
     {
       TTS_RANGE("tts.dist.round");
       ctl.allgather(mine, kRec, st.data(), [&] {
@@ -391,6 +397,7 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
       gbest = std::min<int>(gbest, static_cast<int>(st[r * kRec + 1]));
       replicated |= st[r * kRec + 2] != 0;
       out_of_time |= st[r * kRec + 3] != 0;
+      gives[r] = st[r * kRec + 4];
       total += sizes[r];
       starving |= sizes[r] < static_cast<int64_t>(o.needy_below);
     }
@@ -407,7 +414,9 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
       break;
     }
     if (share && starving && !replicated) {
-      Plan plan = plan_transfers(sizes, o.needy_below, o.donor_min, o.steal_cap, o.local_world, o.intra, o.inter);
+      const size_t nw = sizes.size();
+      Plan plan = plan_transfers(sizes, std::vector<size_t>(nw, o.needy_below), std::vector<size_t>(nw, o.donor_min),
+                                 std::vector<size_t>(nw, o.steal_cap), o.local_world, o.intra, o.inter, &gives);
       if (o.fault_steal_fail_pct && !plan.empty()) {
         std::mt19937_64 rng(o.fault_seed * 1000003ull + rounds);  // same draw on every rank
         Plan kept;

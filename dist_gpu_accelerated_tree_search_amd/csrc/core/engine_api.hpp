@@ -110,6 +110,9 @@ class IEngine {
   virtual void set_overlap(bool on) { (void)on; }
   virtual bool in_flight() { return false; }
   virtual size_t size_known() { return size(); }
+  // ... and what export_device can take right now without waiting for work in flight
+  // (the round plan's cap on this rank as a donor)
+  virtual size_t size_exportable() { return size_known(); }
   virtual int best_known() { return best(); }
   virtual bool split_pending_known() { return split_pending(); }
   virtual void offer_best(int b) {

@@ -103,6 +103,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     TTS_HIP_CHECK(hipEventCreateWithFlags(&up_done_, hipEventDisableTiming));
     TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_comp_, hipEventDisableTiming));
     TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_xfer_, hipEventDisableTiming));
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_ahead_, hipEventDisableTiming));
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&xfer_, hipStreamNonBlocking));
     std::memset(h_ctl_, 0, sizeof(dev::PoolCtl));
     h_ctl_->best.v = 0x7fffffff;
@@ -266,6 +267,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     (void)hipEventDestroy(up_done_);
     (void)hipEventDestroy(ev_comp_);
     (void)hipEventDestroy(ev_xfer_);
+    (void)hipEventDestroy(ev_ahead_);
     if (xfer_) (void)hipStreamDestroy(xfer_);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
     graphs_[0][0].clear();
@@ -416,9 +418,18 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   // With a replay in flight: what can be exported from under it (export_ahead) — the
   // ring part the running replays cannot reach — so a plan built on this size never
   // asks for more than the pool can give without waiting; at least 1 (the replay is work).
+  // With a replay in flight: the pool as of the last completed replay (plus the host
+  // spill), the size the round's needy / donor / termination decisions use (at least 1:
+  // the replay is work), and separately what can be exported from under the running
+  // replays without waiting (export_ahead), the cap on what the plan asks of this rank.
   size_t size_known() override {
     if (inflight_.empty()) return size();
-    return std::max<size_t>(exportable_ahead(), 1);
+    const size_t held = dev_total() + spill_.size() + refill_n_;
+    return std::max<size_t>(held > export_pending_ ? held - export_pending_ : 0, 1);
+  }
+  size_t size_exportable() override {
+    if (inflight_.empty()) return size();
+    return exportable_ahead();
   }
   int best_known() override { return std::min(h_ctl_->best.v, pending_best_); }
   unsigned long long tree_known() override {
@@ -563,8 +574,11 @@ class DeviceEngine final : public IEngine, public DeviceResource {
         const bool budget_ok = !hook_stop && (max_launches < 0 || launches < max_launches) &&
                                (max_seconds <= 0 || elapsed() < max_seconds);
         // overlapped rounds: the slice ends with the last pipelined replay still running
+        // (only a replay short enough that half of the pool stays exportable from under
+        // it, as leave_one's: a long one would hide a donor's pool from the plan)
         if (overlap_ && !budget_ok && inflight_.size() == 1 && (max_launches < 0 || launches < max_launches) &&
-            leave_ok(known)) {
+            leave_ok(known) &&
+            static_cast<size_t>(inflight_k_.front()) <= std::max<size_t>(6, known / 2 / cfg_.max_parents)) {
           leaving = true;
           ++stats_.left_inflight;
           break;
@@ -821,12 +835,21 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (first < n)
       TTS_HIP_CHECK(hipMemcpyAsync(dst + first, d_ring_, (n - first) * sizeof(Node), hipMemcpyDeviceToDevice, xfer_));
     export_pending_ += n;
+    // the ring span is handed back to the compute stream only after this copy
+    // (commit_export makes the stream wait for it: a replay that wraps around the ring
+    // must not overwrite nodes still being copied out behind a slow transfer queue)
+    TTS_HIP_CHECK(hipEventRecord(ev_ahead_, xfer_));
+    ahead_copy_ = true;
     ++stats_.exports;
     ++stats_.overlapped_exports;
     return true;
   }
   void commit_export() {
     if (!export_pending_ || !inflight_.empty()) return;
+    if (ahead_copy_) {
+      TTS_HIP_CHECK(hipStreamWaitEvent(stream_, ev_ahead_, 0));
+      ahead_copy_ = false;
+    }
     h_ctl_->bot = (h_ctl_->bot + export_pending_) & (cap_ - 1);
     h_ctl_->slot[0].stack -= export_pending_;
     export_pending_ = 0;
@@ -1275,6 +1298,8 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   bool learn_first_ = true;  // first replay after begin() = the previous solve's iterations (TTS_LEARN_FIRST=0: off)
   int learned_k_ = 0;     // ... rounded up to 3k (0: unknown)
   std::vector<void*> owned_;
+  hipEvent_t ev_ahead_ = nullptr;  // after the latest export_ahead copy (transfer stream)
+  bool ahead_copy_ = false;
   static constexpr size_t kIlogWords = 8 + 8 * 4095;
   std::string ilog_path_;
   PinnedSpill<Node> spill_;

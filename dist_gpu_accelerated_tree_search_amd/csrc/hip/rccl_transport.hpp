@@ -65,6 +65,15 @@ class RcclTransport final : public DeviceResource {
         (void)hipFree(buf_[b]);
         buf_[b] = nullptr;
       }
+    if (dctl_) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(dctl_);
+      dctl_ = nullptr;
+    }
+    if (hctl_) (void)hipHostFree(hctl_);
+    hctl_ = nullptr;
+    if (own_) (void)hipStreamDestroy(own_);
+    own_ = nullptr;
     if (comm_) (void)ncclCommDestroy(comm_);
     comm_ = nullptr;
   }
@@ -112,6 +121,39 @@ class RcclTransport final : public DeviceResource {
     bytes_recv_ += nin * nb;
     return {nout, nin};
   }
+
+  // Round status all-gather on the communicator (the control plane off the node-local
+  // shm board: several nodes, or TTS_SHM_CONTROL=0; ref MPI_Allreduce / MPI_Allgather of
+  // the comm thread, pfsp_dist_multigpu_cuda.c:69-88,372,385): this rank's n values go
+  // to a device buffer, one in-place ncclAllGather runs on the engine's transfer stream
+  // — after the previous round's send / recv there, so two collectives of this
+  // communicator are never in flight at once — and the host waits for the gathered
+  // (world, n) block to land in pinned memory. No Python, no second communicator.
+  void allgather_i64(const int64_t* v, int n, int64_t* out, IEngine& e) {
+    if (released_) throw std::runtime_error("RCCL transport closed");
+    if (n < 0 || n > kCtlVals) throw std::invalid_argument("RcclTransport::allgather_i64: at most 16 values");
+    TTS_HIP_CHECK(hipSetDevice(device_));
+    hipStream_t xs = reinterpret_cast<hipStream_t>(e.transfer_stream());
+    if (!xs) xs = ctl_stream();
+    if (!dctl_) {
+      TTS_HIP_CHECK(hipMalloc(&dctl_, static_cast<size_t>(world_) * kCtlVals * sizeof(int64_t)));
+      TTS_HIP_CHECK(hipHostMalloc(&hctl_, static_cast<size_t>(world_) * kCtlVals * sizeof(int64_t), hipHostMallocDefault));
+    }
+    if (n == 0) {
+      TTS_HIP_CHECK(hipStreamSynchronize(xs));
+      return;
+    }
+    std::memcpy(hctl_ + static_cast<size_t>(rank_) * n, v, sizeof(int64_t) * n);
+    TTS_HIP_CHECK(hipMemcpyAsync(dctl_ + static_cast<size_t>(rank_) * n, hctl_ + static_cast<size_t>(rank_) * n,
+                                 sizeof(int64_t) * n, hipMemcpyHostToDevice, xs));
+    TTS_NCCL_CHECK(ncclAllGather(dctl_ + static_cast<size_t>(rank_) * n, dctl_, static_cast<size_t>(n), ncclInt64,
+                                 comm_, xs));
+    TTS_HIP_CHECK(hipMemcpyAsync(hctl_, dctl_, sizeof(int64_t) * n * world_, hipMemcpyDeviceToHost, xs));
+    TTS_HIP_CHECK(hipStreamSynchronize(xs));
+    std::memcpy(out, hctl_, sizeof(int64_t) * n * world_);
+    ++collectives_;
+  }
+  unsigned long long collectives() const { return collectives_; }
 
   // World-1 check of the whole path on one GPU: n nodes go pool -> staging -> RCCL send
   // to self / receive from self -> staging -> pool. Returns the nodes moved.
@@ -218,12 +260,37 @@ class RcclTransport final : public DeviceResource {
     return buf_[which];
   }
 
+  hipStream_t ctl_stream() {
+    if (!own_) TTS_HIP_CHECK(hipStreamCreateWithFlags(&own_, hipStreamNonBlocking));
+    return own_;
+  }
+  static constexpr int kCtlVals = 16;
+  int64_t* dctl_ = nullptr;   // (world, n) gathered status, device
+  int64_t* hctl_ = nullptr;   // pinned host image
+  hipStream_t own_ = nullptr;  // for engines without a transfer stream
+  unsigned long long collectives_ = 0;
   ncclComm_t comm_ = nullptr;
   bool released_ = false;
   int rank_, world_, device_;
   void* buf_[2] = {nullptr, nullptr};
   size_t cap_[2] = {0, 0};
   unsigned long long transfers_ = 0, bytes_sent_ = 0, bytes_recv_ = 0;
+};
+
+// The round loop's control plane over the RCCL communicator (no shm board): the status
+// all-gather and the final reductions of run_dist_rounds are ncclAllGather calls.
+class RcclRoundControl final : public RoundControl {
+ public:
+  RcclRoundControl(RcclTransport* t, IEngine* e) : t_(t), e_(e) {}
+  int rank() const override { return t_->rank(); }
+  int world() const override { return t_->world(); }
+  void allgather(const int64_t* v, int n, int64_t* out, const std::function<void()>&) override {
+    t_->allgather_i64(v, n, out, *e_);
+  }
+
+ private:
+  RcclTransport* t_;
+  IEngine* e_;
 };
 
 }  // namespace tts

@@ -224,6 +224,30 @@ class Comm:
             return self.rccl
         return lambda plan: self.execute_transfers(plan, engine, node_bytes)
 
+    def round_allgather(self, engine):
+        """The round loop's status all-gather when there is no shm board (several nodes,
+        TTS_SHM_CONTROL=0): the native RCCL transport for a GPU engine with a transfer
+        stream — ncclAllGather on that stream, after the previous round's send / recv, so
+        the communicator never has two collectives in flight and no Python runs per
+        round — else the process group's all-gather (allgather_i64). Set
+        TTS_RCCL_CONTROL=0 for the process-group path."""
+        if (self.rccl is not None and int(getattr(engine, "transfer_stream", 0) or 0)
+                and os.environ.get("TTS_RCCL_CONTROL", "1") != "0"):
+            return self.rccl
+        xs = int(getattr(engine, "transfer_stream", 0) or 0)
+        if self.rccl is not None and xs:
+            # the process group is a second communicator: let the native transport's
+            # send / recv of the previous round finish first (NCCL: two communicators in
+            # flight on the same GPUs can deadlock)
+            stream = self.torch.cuda.ExternalStream(xs, device=self.device)
+
+            def allgather_after_transfers(values):
+                stream.synchronize()
+                return self.allgather_i64(values)
+
+            return allgather_after_transfers
+        return self.allgather_i64
+
     def _connect_peers(self) -> None:
         """RCCL sets up a point-to-point channel on first use; do it for every pair now
         (one grouped send/recv of one byte per peer), outside any timed region."""

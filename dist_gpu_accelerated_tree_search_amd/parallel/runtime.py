@@ -256,7 +256,7 @@ def _rounds(model, engine, comm: Comm, cfg: DistConfig, t_start: float, t_init: 
     shm = comm.control_address(mod)
     # GPU ranks over RCCL: the native transport, no Python in the loop
     xfer = comm.transport(engine, model.node_bytes) if comm.rccl is not None else transfer
-    out = mod.dist_rounds(engine, shm, None if shm else comm.allgather_i64, rank, world, opts, xfer,
+    out = mod.dist_rounds(engine, shm, None if shm else comm.round_allgather(engine), rank, world, opts, xfer,
                           hook if cfg.checkpoint_dir else None, int(rounds0), float(comm.timeout_s))
     t_search = time.perf_counter() - t_loop
     cnt, tms = out["counts"], out["times"]
@@ -343,7 +343,7 @@ class DistSolver:
         # and the round-robin share (ref roundRobin_distribution)
         warm = cfg.init_per_rank if split else world * cfg.init_per_rank
         self._xfer = comm.transport(engine, model.node_bytes)  # kept alive with the session
-        self._s = mod.DistSession(engine, model, shm, None if shm else comm.allgather_i64, comm.rank, world, opts,
+        self._s = mod.DistSession(engine, model, shm, None if shm else comm.round_allgather(engine), comm.rank, world, opts,
                                   self._xfer, None,
                                   int(warm), int(cfg.split_per_rank * world), float(comm.timeout_s), bool(split))
 

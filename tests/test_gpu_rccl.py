@@ -43,3 +43,22 @@ def test_rccl_self_loop_keeps_golden_tree():
     assert moved > 0
     assert (st["tree"] + t1, st["sol"] + s1, st["best"]) == (2573652, 2648, 1377)
     assert t.rank == 0 and t.world == 1
+
+
+def test_rccl_round_control_world1():
+    # the control plane off the shm board: the round loop's status all-gather and final
+    # reductions as ncclAllGather on the engine's transfer stream (world-1 communicator)
+    import torch  # noqa: F401
+
+    H = ops.require_gpu(0)
+    t = H.RcclTransport(H.RcclTransport.new_id(), 0, 1, 0)
+    model = PfspModel(14, 1)
+    eng = model.make_engine("gpu", 0, EngineOptions(max_parents=1 << 14, ring_bytes=1 << 30))
+    assert t.allgather_i64([7, -3, 1 << 40], eng).tolist() == [[7, -3, 1 << 40]]
+    nodes, t1, s1, best = model.warmup(1377, 25)
+    eng.begin(nodes, best)
+    before = t.collectives
+    out = H.dist_rounds(eng, 0, t, 0, 1, {}, t)
+    assert t.collectives > before + 1  # status rounds + the final reductions
+    assert (int(out["counts"][:, 0].sum()) + t1, int(out["counts"][:, 1].sum()) + s1, out["best"]) == \
+        (2573652, 2648, 1377)

@@ -47,3 +47,19 @@ def test_p2p_calls_match_across_ranks(world):
                     pos += n
         # totals equal what the plan moves
         assert sum(c[3] for r in calls for c in calls[r] if c[0] == "send") == sum(t[2] for t in plan)
+
+
+def test_plan_caps_donation_at_exportable_amount():
+    # a rank with a replay in flight reports its real pool (8000: a donor) and what it
+    # can export without waiting (1000): the plan asks no more than that of it
+    C = ops.cpu()
+    sizes = [8000, 0, 6000, 0]
+    free = C.plan_transfers(sizes, 1000, 2000, 100000)
+    assert free == [(0, 1, 4000), (2, 3, 3000)]
+    capped = C.plan_transfers(sizes, 1000, 2000, 100000, give=[1000, 0, 6000, 0])
+    assert capped == [(0, 1, 1000), (2, 3, 3000)]
+    # the cap is per donor over the whole plan: a second receiver gets the rest of it
+    twice = C.plan_transfers([9000, 0, 0], 1000, 2000, 100000, give=[3000, 0, 0])
+    assert twice == [(0, 1, 3000)]
+    with pytest.raises(ValueError):
+        C.plan_transfers(sizes, 1000, 2000, 100000, give=[1, 2])
