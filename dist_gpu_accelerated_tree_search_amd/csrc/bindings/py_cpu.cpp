@@ -216,6 +216,23 @@ PYBIND11_MODULE(_tts_cpu, m) {
       py::arg("N"), py::arg("G") = 1, py::arg("threads") = 0, py::arg("m") = 25, py::arg("batch") = 20000,
       py::arg("steal_cap") = 250000, py::arg("ws") = true, py::arg("verbose") = false);
 
+  m.def(
+      "pfsp_dive",
+      [](const PfspInstance& in, int beam) {
+        py::gil_scoped_release nogil;
+        return pfsp_dive_makespan(in, beam);
+      },
+      py::arg("inst"), py::arg("beam") = 32,
+      "Makespan of the best complete schedule a beam dive of LB1 reaches (initial incumbent for -u 0).");
+  m.def(
+      "pfsp_neh",
+      [](const PfspInstance& in, long long budget, unsigned seed) {
+        py::gil_scoped_release nogil;
+        PfspNeh h(in);
+        return h.solve(budget, seed);
+      },
+      py::arg("inst"), py::arg("budget") = 5000000LL, py::arg("seed") = 12345u,
+      "NEH + iterated greedy makespan (a complete schedule's) within `budget` cell updates.");
   // ---- Step 1 (BFS warm-up) and Step 3 (DFS drain) for the GPU/distributed drivers ----
   m.def(
       "pfsp_bfs",

@@ -8,6 +8,8 @@
 // CPU workers (-C 1), and are the oracle every GPU kernel is tested against.
 #pragma once
 
+#include <utility>
+
 #include <algorithm>
 #include <climits>
 #include <cstdint>
@@ -196,5 +198,179 @@ inline int cpu_makespan(const PfspInstance& in, const Id* perm) {
   }
   return front[M - 1];
 }
+
+
+// Beam dive for an initial incumbent of a search started without one (-u 0): from the
+// root, keep the `beam` partial schedules of smallest LB1 at every depth (their children
+// bounded incrementally, LB1_d) down to complete schedules, and return the best makespan
+// reached (a leaf's bound is its makespan). The reference's -u 0 search starts from
+// INT_MAX and its depth-first order reaches leaves at once (ref pfsp_c.c:55-63); a
+// breadth-first device window reaches none for tens of millions of nodes, so the
+// device drivers start from this dive's value instead. O(N * beam * N * M).
+inline int pfsp_dive_makespan(const PfspInstance& in, int beam) {
+  const int N = in.jobs;
+  if (N <= 0) return 0;
+  beam = std::max(1, beam);
+  struct Cand {
+    int lb;
+    std::vector<int16_t> prmu;
+  };
+  std::vector<Cand> cur(1);
+  cur[0].lb = 0;
+  cur[0].prmu.resize(N);
+  for (int j = 0; j < N; ++j) cur[0].prmu[j] = static_cast<int16_t>(j);
+  std::vector<int> lbj(N);
+  for (int d = 0; d < N; ++d) {
+    std::vector<Cand> nxt;
+    nxt.reserve(static_cast<size_t>(cur.size()) * (N - d));
+    for (const Cand& c : cur) {
+      cpu_lb1_children(in, c.prmu.data(), d, lbj.data());
+      for (int k = d; k < N; ++k) {
+        Cand x{lbj[c.prmu[k]], c.prmu};
+        std::swap(x.prmu[d], x.prmu[k]);
+        nxt.push_back(std::move(x));
+      }
+    }
+    const size_t keep = std::min<size_t>(static_cast<size_t>(beam), nxt.size());
+    std::partial_sort(nxt.begin(), nxt.begin() + static_cast<std::ptrdiff_t>(keep), nxt.end(),
+                      [](const Cand& a, const Cand& b) { return a.lb < b.lb; });
+    nxt.resize(keep);
+    cur = std::move(nxt);
+  }
+  int best = cur[0].lb;
+  for (const Cand& c : cur) best = std::min(best, c.lb);
+  return best;
+}
+
+
+// ---- Constructive incumbent for -u 0: NEH + iterated greedy (host, deterministic) ----
+// NEH (Nawaz, Enscore, Ham 1983): jobs by decreasing total processing time, each
+// inserted where the partial sequence's makespan is smallest, every position priced at
+// once from the sequence's heads / tails (Taillard 1990, O(L * M) per insertion); then
+// iterated greedy (Ruiz, Stuetzle 2007): remove d jobs, re-insert them greedily, improve
+// by insertion local search, keep the result when it is not worse, until `budget` cell
+// updates are spent. Returns the best makespan (a complete schedule's: >= the optimum).
+class PfspNeh {
+ public:
+  explicit PfspNeh(const PfspInstance& in) : in_(in), N_(in.jobs), M_(in.machines) {}
+
+  int makespan(const std::vector<int>& seq) const {
+    std::vector<int> c(static_cast<size_t>(M_), 0);
+    for (int j : seq)
+      for (int k = 0; k < M_; ++k) c[k] = std::max(c[k], k ? c[k - 1] : 0) + p(k, j);
+    return M_ ? c[M_ - 1] : 0;
+  }
+
+  // best position of job `job` in `seq` and the makespan there
+  std::pair<int, int> best_insert(const std::vector<int>& seq, int job) {
+    const int L = static_cast<int>(seq.size());
+    e_.assign(static_cast<size_t>(L + 1) * M_, 0);
+    q_.assign(static_cast<size_t>(L + 2) * M_, 0);
+    for (int i = 0; i < L; ++i)
+      for (int k = 0; k < M_; ++k)
+        E(i + 1, k) = std::max(E(i, k), k ? E(i + 1, k - 1) : 0) + p(k, seq[i]);
+    for (int i = L - 1; i >= 0; --i)
+      for (int k = M_ - 1; k >= 0; --k)
+        Q(i, k) = std::max(Q(i + 1, k), k + 1 < M_ ? Q(i, k + 1) : 0) + p(k, seq[i]);
+    int best = INT32_MAX, pos = 0;
+    for (int i = 0; i <= L; ++i) {
+      int f = 0, cmax = 0;
+      for (int k = 0; k < M_; ++k) {
+        f = std::max(f, E(i, k)) + p(k, job);
+        cmax = std::max(cmax, f + Q(i, k));
+      }
+      if (cmax < best) {
+        best = cmax;
+        pos = i;
+      }
+    }
+    cells_ += static_cast<long long>(3 * (L + 1)) * M_;
+    return {pos, best};
+  }
+
+  std::vector<int> neh() {
+    std::vector<int> order(static_cast<size_t>(N_));
+    for (int j = 0; j < N_; ++j) order[j] = j;
+    std::vector<long> tot(static_cast<size_t>(N_), 0);
+    for (int j = 0; j < N_; ++j)
+      for (int k = 0; k < M_; ++k) tot[j] += p(k, j);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tot[a] > tot[b]; });
+    std::vector<int> seq;
+    for (int j : order) {
+      const auto bi = best_insert(seq, j);
+      seq.insert(seq.begin() + bi.first, j);
+    }
+    return seq;
+  }
+
+  // insertion local search: every job in turn removed and re-inserted at its best place
+  int local_search(std::vector<int>& seq, int cur) {
+    for (bool improved = true; improved;) {
+      improved = false;
+      for (int t = 0; t < N_; ++t) {
+        const int j = seq[static_cast<size_t>(t)];
+        std::vector<int> rest = seq;
+        rest.erase(rest.begin() + t);
+        const auto bi = best_insert(rest, j);
+        if (bi.second < cur) {
+          rest.insert(rest.begin() + bi.first, j);
+          seq.swap(rest);
+          cur = bi.second;
+          improved = true;
+        }
+      }
+    }
+    return cur;
+  }
+
+  int solve(long long budget, unsigned seed = 12345u) {
+    if (N_ == 0) return 0;
+    std::vector<int> seq = neh();
+    int cur = local_search(seq, makespan(seq));
+    std::vector<int> best_seq = seq;
+    int best = cur;
+    const int d = std::min(4, std::max(1, N_ / 2));
+    unsigned long long x = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&](int n) {
+      x ^= x << 13;
+      x ^= x >> 7;
+      x ^= x << 17;
+      return static_cast<int>(x % static_cast<unsigned long long>(n));
+    };
+    while (cells_ < budget && N_ > 1) {
+      std::vector<int> s2 = seq, removed;
+      for (int r = 0; r < d; ++r) {
+        const int at = rnd(static_cast<int>(s2.size()));
+        removed.push_back(s2[static_cast<size_t>(at)]);
+        s2.erase(s2.begin() + at);
+      }
+      int c2 = 0;
+      for (int j : removed) {
+        const auto bi = best_insert(s2, j);
+        s2.insert(s2.begin() + bi.first, j);
+        c2 = bi.second;
+      }
+      c2 = local_search(s2, c2);
+      if (c2 <= cur) {  // accept equal moves: walks plateaus
+        seq.swap(s2);
+        cur = c2;
+        if (cur < best) {
+          best = cur;
+          best_seq = seq;
+        }
+      }
+    }
+    return best;
+  }
+
+ private:
+  int p(int k, int j) const { return in_.p[static_cast<size_t>(k) * N_ + j]; }
+  int& E(int i, int k) { return e_[static_cast<size_t>(i) * M_ + k]; }
+  int& Q(int i, int k) { return q_[static_cast<size_t>(i) * M_ + k]; }
+  const PfspInstance& in_;
+  int N_, M_;
+  std::vector<int> e_, q_;
+  long long cells_ = 0;
+};
 
 }  // namespace tts

@@ -30,6 +30,9 @@ class QueensModel:
     def initial_best(self, ub: int = 1) -> int:  # no incumbent in a counting problem
         return 0
 
+    def search_best(self, ub: int = 1) -> int:
+        return 0
+
     def root(self) -> np.ndarray:
         return nodes_mod.queens_pack([0], [0], [0], [0])
 

@@ -16,6 +16,7 @@ the CPU and the GPU backends (same engine contract, csrc/core/engine_api.hpp).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -100,6 +101,7 @@ class PfspModel:
         self.jobs = self.native.jobs
         self.machines = self.native.machines
         self.best_known = self.native.best_known
+        self._dive = None  # search_best(0): the beam dive's makespan, computed once
         # engines' node layout: front nodes (depth, unscheduled set, per-machine
         # completion times; csrc/core/pfsp_front.hpp) for LB1 / LB1_d on instances of
         # up to 20 jobs, the permutation node of the job-count bucket otherwise
@@ -114,6 +116,24 @@ class PfspModel:
     def initial_best(self, ub: int = 1) -> int:
         """-u 1: best-known makespan (deterministic tree); -u 0: +inf."""
         return self.best_known if ub == 1 else INT_MAX
+
+    def search_best(self, ub: int = 1) -> int:
+        """Initial incumbent of a device / distributed search: -u 1 as initial_best; -u 0
+        the best complete schedule of two host heuristics (csrc/core/pfsp_bounds_cpu.hpp):
+        a beam dive of LB1 and NEH + iterated greedy (TTS_NEH_BUDGET cell updates, ~5 ms),
+        so the breadth-first device windows prune from the first iteration (ta014 -u 0
+        explored 632 M nodes from +inf, profiles/r4/live_best_u0.txt). TTS_DIVE=0 starts
+        from +inf as the reference does; TTS_DIVE=<beam> sets the beam width (default 32)."""
+        if ub == 1:
+            return self.best_known
+        beam = int(os.environ.get("TTS_DIVE", "32"))
+        if beam <= 0:
+            return INT_MAX
+        if self._dive is None:
+            C = ops.cpu()
+            budget = int(os.environ.get("TTS_NEH_BUDGET", str(5_000_000)))
+            self._dive = min(int(C.pfsp_dive(self.native, beam)), int(C.pfsp_neh(self.native, budget)))
+        return self._dive
 
     # ---- host steps ----
     def root(self) -> np.ndarray:

@@ -125,7 +125,7 @@ def distributed_solve(model, engine, comm: Comm, ub: int = 1, cfg: DistConfig | 
     t_start = time.perf_counter()
 
     # ---- Step 1: redundant, deterministic warm-up on every rank ----
-    best = model.initial_best(ub)
+    best = model.search_best(ub)
     if cfg.resume:
         if not cfg.checkpoint_dir:
             raise ValueError("resume needs checkpoint_dir")
@@ -349,7 +349,7 @@ class DistSolver:
 
     def solve_raw(self, ub: int = 1) -> tuple:
         """(best, tree, sol, rounds, complete, t_init, t_search, elapsed), global values."""
-        return self._s.solve(int(self.model.initial_best(ub)))
+        return self._s.solve(int(self.model.search_best(ub)))
 
     def solve(self, ub: int = 1) -> SolveResult:
         best, tree, sol, rounds, complete, t_init, t_search, elapsed = self.solve_raw(ub)

@@ -73,7 +73,7 @@ def solve_engine(model, engine, ub: int = 1, m: int = 25, best: int | None = Non
     The engine is reused across solves (allocation and graph capture are setup,
     like model initialisation); its counters are reset here."""
     t0 = time.perf_counter()
-    best = model.initial_best(ub) if best is None else best
+    best = model.search_best(ub) if best is None else best
     nodes, tree1, sol1, best = model.warmup(best, m)
     t1 = time.perf_counter()
     if verbose:
@@ -138,7 +138,7 @@ def solve_workers(model, devices=(0,), cpu_threads: int = 0, ub: int = 1, m: int
     if W == 0:
         raise ValueError("no worker")
     t0 = time.perf_counter()
-    best = model.initial_best(ub)
+    best = model.search_best(ub)
     nodes, tree1, sol1, best = model.warmup(best, W * m)
     from .parallel.runtime import round_robin_share
 

@@ -65,7 +65,8 @@ def test_live_incumbent_with_unknown_optimum(world):
     for live in (False, True):
         spec = {"problem": "pfsp", "inst": 2, "lb": 0, "backend": "cpu", "ub": 0, "session": True,
                 "dist": {"live_best": live}}
-        res = spawn_local(world, solve_rank, (spec,), timeout=300)
+        # no dive: every rank starts from +inf, so incumbents really have to travel
+        res = spawn_local(world, solve_rank, (spec,), timeout=300, env={"TTS_DIVE": "0"})
         assert all(r["best"] == 1359 for r in res)
         trees[live] = res[0]["tree"]
     assert trees[True] > 0 and trees[False] > 0

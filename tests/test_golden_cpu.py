@@ -71,3 +71,46 @@ def test_queens_g_does_not_change_counts():
 def test_queens_14_sequential():
     r = solve_cpu(QueensModel(14))
     assert (r.tree, r.sol) == (27358552, 365596)
+
+
+@pytest.mark.parametrize("inst,beam", [(14, 32), (21, 32), (1, 8), (31, 8)])
+def test_beam_dive_gives_a_real_schedule_makespan(inst, beam):
+    # -u 0 device searches start from the dive's makespan: a complete schedule's, so
+    # never below the optimum (Taillard's best known for these solved instances), and
+    # close to it (within 10 %)
+    import itertools  # noqa: F401
+
+    from dist_gpu_accelerated_tree_search_amd import ops
+    from dist_gpu_accelerated_tree_search_amd.models.pfsp import PfspModel
+
+    m = PfspModel(inst, 1)
+    v = ops.cpu().pfsp_dive(m.native, beam)
+    assert m.best_known <= v <= 1.25 * m.best_known, (v, m.best_known)
+    h = ops.cpu().pfsp_neh(m.native, 2_000_000)  # NEH + iterated greedy: within 3 %
+    assert m.best_known <= h <= 1.03 * m.best_known, (h, m.best_known)
+    assert m.search_best(0) == min(v, ops.cpu().pfsp_neh(m.native, 5_000_000))
+
+
+def test_beam_dive_exact_on_tiny_instances():
+    import itertools
+
+    import numpy as np
+
+    from dist_gpu_accelerated_tree_search_amd import ops
+    from dist_gpu_accelerated_tree_search_amd.models.pfsp import PfspModel
+
+    m = PfspModel.synthetic(7, 4, seed=5, lb=1)
+    p = np.asarray(m.native.p).reshape(4, 7)
+
+    def cmax(perm):
+        c = [0] * 4
+        for j in perm:
+            for k in range(4):
+                c[k] = max(c[k], c[k - 1] if k else 0) + int(p[k, j])
+        return c[-1]
+
+    opt = min(cmax(q) for q in itertools.permutations(range(7)))
+    assert ops.cpu().pfsp_dive(m.native, 5040) == opt  # a beam as wide as the tree is exact
+    assert ops.cpu().pfsp_dive(m.native, 1) >= opt
+    assert ops.cpu().pfsp_neh(m.native, 0) >= opt  # NEH + local search alone
+    assert ops.cpu().pfsp_neh(m.native, 10_000_000) == opt

@@ -81,7 +81,7 @@ def test_gpu_unknown_optimum_multi_rank(live):
     # -u 0 on 2 ranks: the optimum is found with and without the live incumbent exchange
     spec = {"problem": "pfsp", "inst": 14, "lb": 1, "backend": "gpu", "comm": "gloo", "device": 0, "session": True,
             "ub": 0, "engine": {"ring_bytes": 1 << 30, "max_parents": 1 << 16}, "dist": {"live_best": live}}
-    res = spawn_local(2, solve_rank, (spec,), timeout=600)
+    res = spawn_local(2, solve_rank, (spec,), timeout=600, env={"TTS_DIVE": "0"})  # from +inf (no dive)
     assert all(r["best"] == 1377 for r in res)
 
 
