@@ -125,8 +125,8 @@ inline int lb2_pipe_wanted() {
   return f ? (std::atoi(f) != 0) : 1;
 }
 
-// The LB2 kernel with two children per lane in packed u16 walks (LBK 5): job sets
-// of at most two words (<= 128 jobs), and every walk value must fit 16 bits. A walk value (a child
+// The LB2 kernel with two children per lane in packed u16 walks (LBK 5): every walk
+// value must fit 16 bits (any job count: wide job sets read their words from LDS). A walk value (a child
 // front, t0 + p0, t0 + lag, t1 + p1) is the length of a monotone staircase path
 // through the machine x job grid (prefix columns, then Johnson-order columns; a lag
 // is the column segment between the pair's machines), so it visits at most
@@ -134,7 +134,6 @@ inline int lb2_pipe_wanted() {
 // p <= 99: 6,831). The tails are added in 32 bits after the walk. On when it applies
 // unless TTS_LB2_PK=0 (A/B).
 inline bool lb2_pk_ok(const PfspInstance& in) {
-  if (in.jobs > 128) return false;
   long pmax = 0;
   for (int v : in.p) pmax = std::max<long>(pmax, v);
   return (in.jobs + in.machines - 1) * pmax < 65536;
@@ -760,8 +759,7 @@ TTS_PFSP_DECLARE_BUCKET(500)
       if constexpr (NJ == 20)                                                                        \
         if (pfsp_front_ok(in, lb)) return make_pfsp_front_engine_t<M>(in, cfg);                      \
       if (lb != 2) return make_pfsp_engine_t<NJ, M, 1>(in, cfg);                                    \
-      if constexpr (NJ <= 128)                                                                       \
-        if (M >= 10 && lb2_pk_wanted(in)) return make_pfsp_engine_t<NJ, M, 5>(in, cfg);               \
+      if (M >= 10 && lb2_pk_wanted(in)) return make_pfsp_engine_t<NJ, M, 5>(in, cfg);                 \
       return make_pfsp_engine_t<NJ, M, 2>(in, cfg);                                                  \
     });                                                                                              \
   }                                                                                                  \

@@ -492,10 +492,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LBK == 5
 void pfsp_expand_kernel(PfspArgs<NJ, M> a, int t) {
   if constexpr (LBK == 2)
     pfsp_expand_lb2<NJ, M>(a, t);
-  else if constexpr (LBK == 5 && NJ <= 128)
-    pfsp_expand_lb2<NJ, M, true>(a, t);  // two children per lane, packed u16 walks
   else if constexpr (LBK == 5)
-    pfsp_expand_lb2<NJ, M>(a, t);  // (job sets of one word only)
+    pfsp_expand_lb2<NJ, M, true>(a, t);  // two children per lane, packed u16 walks
   else
     pfsp_expand_lb1<NJ, M>(a, t);  // permutation nodes (20-job instances use pfsp_front_kernels.hpp)
 }
@@ -632,8 +630,9 @@ __device__ inline void lb2_walk_pipe(const uint4* rq, int ndouble, const u64 (&m
 // half skips the jobs of its own child's scheduled set (bit field insert on a
 // per-half keep mask). Exact as long as every value of the walk fits 16 bits: a walk
 // value is a path length through the p matrix (host check lb2_pk_ok: (jobs + machines
-// - 1) x max p < 65536). Job sets of NW > 1 words (100-job instances) pick the word
-// of the record's job first (one 64-bit select per word and child).
+// - 1) x max p < 65536: 500 x 20 with p <= 99 gives 51,381). Job sets of two words
+// (100-job instances) pick the word of the record's job by a select per child; wider
+// ones (200 / 500 jobs) read it from LDS (lb2_step2_lds).
 // (u16x2 helpers: device_common.hpp)
 
 template <int NW>
@@ -680,6 +679,46 @@ __device__ inline void lb2_walk_pipe2(const uint4* rq, int ndouble, const u64 (&
     lb2_step2<NW>(b0.z, b0.w, ma, mb, t0, t1);
     lb2_step2<NW>(b1.x, b1.y, ma, mb, t0, t1);
     lb2_step2<NW>(b1.z, b1.w, ma, mb, t0, t1);
+    b0 = rq[4 * g + 6];
+    b1 = rq[4 * g + 7];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Job sets of more than two words (200 / 500-job instances): the word of the record's
+// job is read from the children's LDS rows (one ds_read_b64 per child and step, issued
+// with the record group, independent of the walk's dependence chain) instead of
+// selecting it among NW words held in registers (2 (NW - 1) 64-bit selects per child).
+__device__ inline void lb2_step2_lds(uint32_t x, uint32_t y, const u64* ma, const u64* mb, uint32_t& t0,
+                                     uint32_t& t1) {
+  const u16x2 p0 = static_cast<u16x2>(static_cast<unsigned short>(x >> 16));
+  const u16x2 lag = static_cast<u16x2>(static_cast<unsigned short>(y >> 16));
+  const u16x2 p1 = static_cast<u16x2>(static_cast<unsigned short>(y & 0xffff));
+  const u16x2 n0 = as_u16x2(t0) + p0;
+  const u16x2 n1 = __builtin_elementwise_max(as_u16x2(t1), n0 + lag) + p1;
+  const uint32_t job = x & 63u, wj = (x & 0xffffu) >> 6;
+  const int ka = __builtin_amdgcn_sbfe(static_cast<int>(static_cast<uint32_t>(ma[wj] >> job)), 0, 1);
+  const int kb = __builtin_amdgcn_sbfe(static_cast<int>(static_cast<uint32_t>(mb[wj] >> job)), 0, 1);
+  const uint32_t keep = __builtin_amdgcn_perm(static_cast<uint32_t>(kb), static_cast<uint32_t>(ka), 0x05040100u);
+  t0 = (t0 & keep) | (as_u32(n0) & ~keep);
+  t1 = (t1 & keep) | (as_u32(n1) & ~keep);
+}
+
+__device__ inline void lb2_walk_pipe2_lds(const uint4* rq, int ndouble, const u64* ma, const u64* mb, uint32_t& t0,
+                                          uint32_t& t1) {
+  uint4 a0 = rq[0], a1 = rq[1], b0 = rq[2], b1 = rq[3];
+  for (int g = 0; g < ndouble; ++g) {
+    lb2_step2_lds(a0.x, a0.y, ma, mb, t0, t1);
+    lb2_step2_lds(a0.z, a0.w, ma, mb, t0, t1);
+    lb2_step2_lds(a1.x, a1.y, ma, mb, t0, t1);
+    lb2_step2_lds(a1.z, a1.w, ma, mb, t0, t1);
+    a0 = rq[4 * g + 4];
+    a1 = rq[4 * g + 5];
+    __builtin_amdgcn_sched_barrier(0);
+    lb2_step2_lds(b0.x, b0.y, ma, mb, t0, t1);
+    lb2_step2_lds(b0.z, b0.w, ma, mb, t0, t1);
+    lb2_step2_lds(b1.x, b1.y, ma, mb, t0, t1);
+    lb2_step2_lds(b1.z, b1.w, ma, mb, t0, t1);
     b0 = rq[4 * g + 6];
     b1 = rq[4 * g + 7];
     __builtin_amdgcn_sched_barrier(0);
@@ -820,7 +859,6 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         const int nq = min(P - q0, R);
         if constexpr (PK) {
           // tasks (pair, child pair): children alist[2k], alist[2k + 1] share a lane
-          static_assert(G::NW <= 2, "packed walks: job sets of at most two words");
           const int nk = (na + 1) >> 1;
           int qq = tid / nk, kk = tid - (tid / nk) * nk;
           const int dq = kBlock / nk, dk = kBlock - dq * nk;
@@ -834,13 +872,19 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
               const int cbb = cb >= 0 ? cb : ca;
               uint32_t t0 = static_cast<uint32_t>(sm.cf[m0][ca]) | (static_cast<uint32_t>(sm.cf[m0][cbb]) << 16);
               uint32_t t1 = static_cast<uint32_t>(sm.cf[m1][ca]) | (static_cast<uint32_t>(sm.cf[m1][cbb]) << 16);
-              u64 ma[G::NW], mb[G::NW];
+              if constexpr (G::NW > 2) {
+                // (a lone child walks in both halves; the second half's result is unused)
+                lb2_walk_pipe2_lds(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, sm.cm[ca], sm.cm[cbb],
+                                   t0, t1);
+              } else {
+                u64 ma[G::NW], mb[G::NW];
 #pragma unroll
-              for (int w = 0; w < G::NW; ++w) {
-                ma[w] = sm.cm[ca][w];
-                mb[w] = cb >= 0 ? sm.cm[cbb][w] : ~0ull;
+                for (int w = 0; w < G::NW; ++w) {
+                  ma[w] = sm.cm[ca][w];
+                  mb[w] = cb >= 0 ? sm.cm[cbb][w] : ~0ull;
+                }
+                lb2_walk_pipe2(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, ma, mb, t0, t1);
               }
-              lb2_walk_pipe2(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, ma, mb, t0, t1);
               const int tl0 = static_cast<int>(pi.y & 0xffff), tl1 = static_cast<int>(pi.y >> 16);
               if (la)
                 atomicMax(&sm.lbv[ca], max(static_cast<int>(t1 & 0xffff) + tl1, static_cast<int>(t0 & 0xffff) + tl0));

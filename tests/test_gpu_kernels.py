@@ -67,8 +67,9 @@ def test_queens_labels_match_cpu(N, G):
     assert np.array_equal(model.labels_gpu(nodes), model.labels_cpu(nodes))
 
 
-@pytest.mark.parametrize("inst,best_from", [(3, None), (14, None), (21, None), (56, None), (81, None), (101, None),
-                                            (14, "opt"), (56, "opt"), (21, "opt")])
+@pytest.mark.parametrize("inst,best_from", [(3, None), (14, None), (21, None), (56, None), (81, None), (91, None),
+                                            (101, None), (111, None), (14, "opt"), (56, "opt"), (21, "opt"),
+                                            (111, "opt")])
 @pytest.mark.parametrize("variant", [1, 2, 4])
 def test_lb2_expand_path_matches_cpu(inst, best_from, variant):
     # the production LB2 expand kernel (B1 LB1 filter, learned pair order, B2 walks:
@@ -76,8 +77,8 @@ def test_lb2_expand_path_matches_cpu(inst, best_from, variant):
     # B3 decision) against cpu_lb2 child by child: exact values when best = INT_MAX,
     # the lb < best decision otherwise
     model = PfspModel(inst, 2)
-    if variant == 4 and (model.jobs > 128 or (model.jobs + model.machines - 1) * max(model.native.p) >= 65536):
-        pytest.skip("packed walks need job sets of one word and 16-bit walk values (lb2_pk_ok)")
+    if variant == 4 and (model.jobs + model.machines - 1) * max(model.native.p) >= 65536:
+        pytest.skip("packed walks need 16-bit walk values (lb2_pk_ok)")
     n = {20: 600, 50: 200, 100: 40}.get(model.jobs, 12)
     nodes = random_nodes(model.jobs, n, inst * 7 + variant)
     best = INT_MAX if best_from is None else model.best_known
