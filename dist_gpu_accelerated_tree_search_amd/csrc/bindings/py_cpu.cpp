@@ -154,10 +154,14 @@ PYBIND11_MODULE(_tts_cpu, m) {
           if (!pfsp_front_ok(in, lb)) return nodes_to_array(p, n);
           return with_pfsp_problem(in, lb, [&](auto prob) -> U8 {
             using P = decltype(prob);
-            if constexpr (is_front_problem<P>::value && NJ == 20) {
-              std::vector<typename P::Node> out(n);
-              for (size_t i = 0; i < n; ++i) out[i] = pfsp_front_from_perm(prob, p[i]);
-              return nodes_to_array(out.data(), n);
+            if constexpr (is_front_problem<P>::value) {
+              if constexpr (NJ == P::kJobs) {
+                std::vector<typename P::Node> out(n);
+                for (size_t i = 0; i < n; ++i) out[i] = pfsp_front_from_perm(prob, p[i]);
+                return nodes_to_array(out.data(), n);
+              } else {
+                return nodes_to_array(p, n);
+              }
             } else {
               return nodes_to_array(p, n);
             }
@@ -179,9 +183,9 @@ PYBIND11_MODULE(_tts_cpu, m) {
           const Node* p = array_nodes<Node>(nodes, n);
           for (size_t i = 0; i < n; ++i) {
             if constexpr (is_front_problem<P>::value) {
-              int by_job[32];
+              int by_job[64];
               prob.children_bounds(p[i], by_job);
-              for (uint32_t x = p[i].rest; x; x &= x - 1) out.push_back(by_job[__builtin_ctz(x)]);
+              for (auto x = p[i].rest; x; x &= x - 1) out.push_back(by_job[mask_ctz(x)]);
             } else {
               throw std::invalid_argument("pfsp_children_bounds: front layout only");
             }

@@ -62,38 +62,48 @@ inline PfspPadded pfsp_padded_tables(const PfspInstance& in, int MB) {
   return t;
 }
 
-// The front layout applies: LB1 / LB1_d, at most 20 jobs (the 20-job bucket) and 20
-// machines, and every front fits 16 bits (the sum of all processing times does).
+// The front layout applies: LB1 / LB1_d, at most 50 jobs (job sets of 32 bits up to 20
+// jobs, 64 bits up to 50) and 20 machines, and every front fits 16 bits (the sum of all
+// processing times does).
 // TTS_FRONT=0 turns it off (permutation nodes everywhere: A/B runs); the CPU and the
 // HIP module read the variable alike, so every engine of a process agrees.
 inline bool pfsp_front_ok(const PfspInstance& in, int lb) {
   if (lb != 0 && lb != 1) return false;
   if (const char* e = std::getenv("TTS_FRONT"))
     if (e[0] == '0') return false;
-  if (in.jobs > 20 || in.machines > 20 || pfsp_machine_bucket(in.machines) == 0) return false;
+  if (in.jobs > 50 || in.machines > 20 || pfsp_machine_bucket(in.machines) == 0) return false;
   long tot = 0;
   for (int v : in.p) tot += v;
   return tot < 65536;
 }
 
-template <int MB>
+// job bucket of the front layout: 20 (32-bit job sets) or 50 (64-bit)
+inline int pfsp_front_jobs(int jobs) { return jobs <= 20 ? 20 : 50; }
+
+template <int MB, int NJ = 20>
 struct PfspFrontProblem {
-  using Node = PfspFrontNode<MB>;
+  using Node = PfspFrontNode<MB, NJ>;
+  using Mask = typename Node::Mask;
+  static constexpr int kJobs = NJ;
+  static constexpr int kMaxJ = NJ <= 32 ? 32 : 64;
   const PfspInstance* inst = nullptr;
   int lb = 1;
   int jobs = 0;
   PfspPadded tab{};
-  int p[32][MB];  // job-major, padded machines 0
+  int p[kMaxJ][MB];  // job-major, padded machines 0
 
   PfspFrontProblem(const PfspInstance& in, int lb_kind) : inst(&in), lb(lb_kind), jobs(in.jobs) {
     if (!pfsp_front_ok(in, lb_kind)) throw std::invalid_argument("front layout does not apply to this instance");
     if (pfsp_machine_bucket(in.machines) != MB) throw std::invalid_argument("wrong machine bucket");
+    if (pfsp_front_jobs(in.jobs) != NJ) throw std::invalid_argument("wrong front job bucket");
     tab = pfsp_padded_tables(in, MB);
-    for (int j = 0; j < 32; ++j)
+    for (int j = 0; j < kMaxJ; ++j)
       for (int m = 0; m < MB; ++m) p[j][m] = (j < in.jobs && m < in.machines) ? in.pt(m, j) : 0;
   }
 
-  uint32_t all_jobs() const { return jobs >= 32 ? 0xffffffffu : ((1u << jobs) - 1u); }
+  Mask all_jobs() const {
+    return jobs >= static_cast<int>(8 * sizeof(Mask)) ? ~Mask(0) : ((Mask(1) << jobs) - Mask(1));
+  }
 
   Node root() const {
     Node r{};
@@ -106,8 +116,8 @@ struct PfspFrontProblem {
   // remain + tail of the parent's unscheduled jobs, per machine
   void remain_tail(const Node& n, int* r) const {
     for (int m = 0; m < MB; ++m) r[m] = tab.tails[m];
-    for (uint32_t x = n.rest; x; x &= x - 1) {
-      const int j = __builtin_ctz(x);
+    for (Mask x = n.rest; x; x &= x - 1) {
+      const int j = mask_ctz(x);
       for (int m = 0; m < MB; ++m) r[m] += p[j][m];
     }
   }
@@ -136,8 +146,8 @@ struct PfspFrontProblem {
   void children_bounds(const Node& n, int* lb_by_job) const {
     int r[MB];
     remain_tail(n, r);
-    for (uint32_t x = n.rest; x; x &= x - 1) {
-      const int j = __builtin_ctz(x);
+    for (Mask x = n.rest; x; x &= x - 1) {
+      const int j = mask_ctz(x);
       lb_by_job[j] = child(n, r, j, nullptr);
     }
   }
@@ -147,8 +157,8 @@ struct PfspFrontProblem {
     int r[MB];
     remain_tail(parent, r);
     const bool leaf = parent.depth + 1 == jobs;
-    for (uint32_t x = parent.rest; x; x &= x - 1) {
-      const int j = __builtin_ctz(x);
+    for (Mask x = parent.rest; x; x &= x - 1) {
+      const int j = mask_ctz(x);
       Node c{};
       const int b = child(parent, r, j, leaf ? nullptr : c.front);
       if (leaf) {
@@ -156,7 +166,7 @@ struct PfspFrontProblem {
         if (b < best) best = b;
       } else if (b < best) {
         c.depth = static_cast<uint8_t>(parent.depth + 1);
-        c.rest = parent.rest & ~(1u << j);
+        c.rest = parent.rest & ~(Mask(1) << j);
         push(c);
         ++tree;
       }
@@ -166,13 +176,14 @@ struct PfspFrontProblem {
 
 template <class P>
 struct is_front_problem : std::false_type {};
-template <int MB>
-struct is_front_problem<PfspFrontProblem<MB>> : std::true_type {};
+template <int MB, int NJ>
+struct is_front_problem<PfspFrontProblem<MB, NJ>> : std::true_type {};
 
 // Front node of a permutation node (scheduled prefix prmu[0..depth)).
-template <int MB, class PermNode>
-inline PfspFrontNode<MB> pfsp_front_from_perm(const PfspFrontProblem<MB>& prob, const PermNode& n) {
-  PfspFrontNode<MB> f{};
+template <int MB, int NJ, class PermNode>
+inline PfspFrontNode<MB, NJ> pfsp_front_from_perm(const PfspFrontProblem<MB, NJ>& prob, const PermNode& n) {
+  using Mask = typename PfspFrontNode<MB, NJ>::Mask;
+  PfspFrontNode<MB, NJ> f{};
   f.depth = static_cast<uint8_t>(n.depth);
   f.rest = prob.all_jobs();
   if (n.depth == 0) {
@@ -182,7 +193,7 @@ inline PfspFrontNode<MB> pfsp_front_from_perm(const PfspFrontProblem<MB>& prob, 
   int fr[MB] = {};
   for (int i = 0; i < n.depth; ++i) {
     const int j = n.prmu[i];
-    f.rest &= ~(1u << j);
+    f.rest &= ~(Mask(1) << j);
     fr[0] += prob.p[j][0];
     for (int m = 1; m < MB; ++m) fr[m] = std::max(fr[m - 1], fr[m]) + prob.p[j][m];
   }
@@ -196,10 +207,17 @@ inline PfspFrontNode<MB> pfsp_front_from_perm(const PfspFrontProblem<MB>& prob, 
 template <class F>
 decltype(auto) with_pfsp_problem(const PfspInstance& in, int lb, F&& f) {
   if (pfsp_front_ok(in, lb)) {
+    if (in.jobs <= 20) {
+      switch (pfsp_machine_bucket(in.machines)) {
+        case 5: return f(PfspFrontProblem<5>(in, lb));
+        case 10: return f(PfspFrontProblem<10>(in, lb));
+        default: return f(PfspFrontProblem<20>(in, lb));
+      }
+    }
     switch (pfsp_machine_bucket(in.machines)) {
-      case 5: return f(PfspFrontProblem<5>(in, lb));
-      case 10: return f(PfspFrontProblem<10>(in, lb));
-      default: return f(PfspFrontProblem<20>(in, lb));
+      case 5: return f(PfspFrontProblem<5, 50>(in, lb));
+      case 10: return f(PfspFrontProblem<10, 50>(in, lb));
+      default: return f(PfspFrontProblem<20, 50>(in, lb));
     }
   }
   return with_pfsp_bucket(in.jobs, [&](auto nj) -> decltype(auto) {

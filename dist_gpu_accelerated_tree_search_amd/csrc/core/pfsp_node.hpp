@@ -67,16 +67,27 @@ TTS_HD inline PfspNode<NJ> pfsp_child(const PfspNode<NJ>& parent, int k) {
 //   rest        bit j set: job j is not scheduled yet
 //   front[m]    completion time of the prefix on machine m; at the root the minimum
 //               heads (ref schedule_front with limit1 == -1)
-template <int MB>
+// NJ (job bucket of the front layout): 20 keeps the unscheduled set in 32 bits, 50 in
+// 64 (the set then starts at byte 8 and the fronts at byte 16).
+template <int MB, int NJ = 20>
 struct alignas(16) PfspFrontNode {
   static constexpr int kMachines = MB;
+  static constexpr int kJobs = NJ;
+  using Mask = std::conditional_t<(NJ <= 32), uint32_t, uint64_t>;
   uint8_t depth;
-  uint8_t pad[3];
-  uint32_t rest;
+  uint8_t pad[sizeof(Mask) - 1];
+  Mask rest;
   uint16_t front[MB];
 };
 static_assert(sizeof(PfspFrontNode<5>) == 32 && sizeof(PfspFrontNode<10>) == 32 && sizeof(PfspFrontNode<20>) == 48,
               "front node sizes");
+static_assert(sizeof(PfspFrontNode<5, 50>) == 32 && sizeof(PfspFrontNode<10, 50>) == 48 &&
+                  sizeof(PfspFrontNode<20, 50>) == 64,
+              "50-job front node sizes");
+
+// lowest set bit of a job set (32 or 64 bits)
+TTS_HD inline int mask_ctz(uint32_t x) { return __builtin_ctz(x); }
+TTS_HD inline int mask_ctz(uint64_t x) { return __builtin_ctzll(x); }
 
 // Job-count buckets a run-time instance is dispatched to.
 inline int pfsp_bucket(int jobs) {

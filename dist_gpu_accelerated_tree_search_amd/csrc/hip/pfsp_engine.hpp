@@ -55,11 +55,11 @@ struct PfspTraits {
 };
 
 // LB1 / LB1_d on front-carrying nodes (pfsp_front_kernels.hpp), machine bucket M.
-template <int M>
+template <int M, int NJ = 20>
 struct PfspFrontTraits {
-  using Node = PfspFrontNode<M>;
-  using Args = dev::PfspFrontArgs<M>;
-  using G = dev::FrontGeom<M>;
+  using Node = PfspFrontNode<M, NJ>;
+  using Args = dev::PfspFrontArgs<M, NJ>;
+  using G = dev::FrontGeom<M, NJ>;
   static constexpr int kParentsPerChunk = G::BP;
   static constexpr int kChildrenPerChunk = G::SLOT;
   static constexpr int kMaxChildren = G::NJ;
@@ -72,7 +72,7 @@ struct PfspFrontTraits {
   static constexpr int kMaxChunks = G::MAXCHUNKS;
   static constexpr bool kDyn = true;  // dynamic local DFS iterations (front_dyn)
   static void launch(const Args& a, int t, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
+    hipLaunchKernelGGL((dev::pfsp_front_kernel<M, NJ>), dim3(grid), dim3(dev::kBlock), 0, s, a, t);
   }
   static void flatten(const dev::PoolArgs<Node>& pa, int b, int grid, hipStream_t s) {
     hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::SLOT, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
@@ -83,29 +83,29 @@ struct PfspFrontTraits {
   }
   static int blocks_per_cu() {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_front_kernel<M>, dev::kBlock, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_front_kernel<M, NJ>, dev::kBlock, 0) != hipSuccess)
       return 1;
     return std::min(n, G::WAVES);  // FrontGeom::WAVES: the API over-reports by one
   }
 };
 
 // Front-layout tables: job-major u16 p rows padded to the LDS stride, padded tails.
-template <int M>
-inline std::vector<uint16_t> pfsp_front_fill_args(const PfspInstance& in, dev::PfspFrontArgs<M>& a) {
-  if (!pfsp_front_ok(in, 1) || pfsp_machine_bucket(in.machines) != M)
+template <int M, int NJ>
+inline std::vector<uint16_t> pfsp_front_fill_args(const PfspInstance& in, dev::PfspFrontArgs<M, NJ>& a) {
+  if (!pfsp_front_ok(in, 1) || pfsp_machine_bucket(in.machines) != M || pfsp_front_jobs(in.jobs) != NJ)
     throw std::invalid_argument("front layout does not apply to this instance");
-  constexpr int MS = dev::FrontGeom<M>::MS;
+  constexpr int MS = dev::FrontGeom<M, NJ>::MS;
   const PfspPadded t = pfsp_padded_tables(in, M);
   std::vector<uint16_t> ptab(static_cast<size_t>(in.jobs) * MS, 0);
   for (int j = 0; j < in.jobs; ++j)
     for (int m = 0; m < in.machines; ++m) ptab[static_cast<size_t>(j) * MS + m] = static_cast<uint16_t>(in.pt(m, j));
   a.jobs = in.jobs;
   for (int m = 0; m < M; ++m) a.min_tails[m] = t.tails[m];
-  a.bpf = dev::FrontGeom<M>::BPF;
-  a.cp_max = dev::FrontGeom<M>::CPMAX;
+  a.bpf = dev::FrontGeom<M, NJ>::BPF;
+  a.cp_max = dev::FrontGeom<M, NJ>::CPMAX;
   if (const char* f = std::getenv("TTS_CP_MAX")) a.cp_max = std::max(0, std::atoi(f));  // A/B runs
   if (const char* f = std::getenv("TTS_FUSED_BPF"))  // A/B runs
-    a.bpf = std::min(std::max(1, std::atoi(f)), dev::FrontGeom<M>::BPF_CP);
+    a.bpf = std::min(std::max(1, std::atoi(f)), dev::FrontGeom<M, NJ>::BPF_CP);
   return ptab;
 }
 
@@ -458,13 +458,13 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
   }
 }
 
-template <int M>
+template <int M, int NJ = 20>
 std::unique_ptr<IEngine> make_pfsp_front_engine_t(const PfspInstance& in, const EngineConfig& cfg) {
   TTS_HIP_CHECK(hipSetDevice(cfg.device));
-  dev::PfspFrontArgs<M> a{};
+  dev::PfspFrontArgs<M, NJ> a{};
   const std::vector<uint16_t> ptab = pfsp_front_fill_args(in, a);
   a.ptab = upload_vec(ptab);
-  auto eng = std::make_unique<DeviceEngine<PfspFrontTraits<M>>>(cfg, a);
+  auto eng = std::make_unique<DeviceEngine<PfspFrontTraits<M, NJ>>>(cfg, a);
   eng->adopt(const_cast<uint16_t*>(a.ptab));
   return eng;
 }
@@ -485,15 +485,15 @@ struct FrontProbeResult {
   EngineStats st;
   std::vector<uint32_t> first_bad;
 };
-template <int M>
+template <int M, int NJ = 20>
 FrontProbeResult pfsp_front_probe_t(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
                                     const EngineConfig& cfg, unsigned cap, int split_rank, int split_world,
                                     size_t split_min) {
-  using G = dev::FrontGeom<M>;
-  using Node = PfspFrontNode<M>;
+  using G = dev::FrontGeom<M, NJ>;
+  using Node = PfspFrontNode<M, NJ>;
   TTS_HIP_CHECK(hipSetDevice(cfg.device));
-  const PfspFrontProblem<M> prob(in, lb);
-  dev::PfspFrontArgs<M> a{};
+  const PfspFrontProblem<M, NJ> prob(in, lb);
+  dev::PfspFrontArgs<M, NJ> a{};
   const std::vector<uint16_t> ptab = pfsp_front_fill_args(in, a);
   a.ptab = upload_vec(ptab);
   uint32_t* drec = nullptr;
@@ -506,7 +506,7 @@ FrontProbeResult pfsp_front_probe_t(const PfspInstance& in, int lb, const void* 
   a.dbg_cap = cap;
   FrontProbeResult res;
   {
-    DeviceEngine<PfspFrontTraits<M>> eng(cfg, a);
+    DeviceEngine<PfspFrontTraits<M, NJ>> eng(cfg, a);
     if (split_world > 1) eng.set_split(split_rank, split_world, split_min);
     res.st = eng.solve_from(nodes, n, best);
   }
@@ -556,14 +556,14 @@ FrontProbeResult pfsp_front_probe_t(const PfspInstance& in, int lb, const void* 
 // ms), then one launch with the per-workgroup phase stamps (front_stamp). Returns
 // {ms_min, ms_median, grid, iteration levels, then grid x 16 stamps in us from the first
 // workgroup entry (0 where a stamp was not reached)}.
-template <int M>
+template <int M, int NJ = 20>
 std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
                                       const EngineConfig& cfg, int reps) {
-  using G = dev::FrontGeom<M>;
-  using Node = PfspFrontNode<M>;
+  using G = dev::FrontGeom<M, NJ>;
+  using Node = PfspFrontNode<M, NJ>;
   TTS_HIP_CHECK(hipSetDevice(cfg.device));
   (void)lb;
-  dev::PfspFrontArgs<M> a{};
+  dev::PfspFrontArgs<M, NJ> a{};
   const std::vector<uint16_t> ptab = pfsp_front_fill_args(in, a);
   std::vector<void*> owned;
   auto dalloc = [&](size_t bytes) {
@@ -607,7 +607,7 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   pa.wide_levels = cfg.wide_levels;
   if (const char* f = std::getenv("TTS_WIDE_LEVELS")) pa.wide_levels = std::atoi(f);
   int bpc = 0, cus = 0;
-  bpc = PfspFrontTraits<M>::blocks_per_cu();
+  bpc = PfspFrontTraits<M, NJ>::blocks_per_cu();
   if (const char* g = std::getenv("TTS_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(g));  // as DeviceEngine
   TTS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device));
   const int grid = static_cast<int>(std::min<size_t>(max_chunks, static_cast<size_t>(std::max(1, bpc)) * cus));
@@ -634,7 +634,7 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   for (int r = 0; r < std::max(1, reps); ++r) {
     restore();
     TTS_HIP_CHECK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, 0, a, 0);
+    hipLaunchKernelGGL((dev::pfsp_front_kernel<M, NJ>), dim3(grid), dim3(dev::kBlock), 0, 0, a, 0);
     TTS_HIP_CHECK(hipGetLastError());
     TTS_HIP_CHECK(hipEventRecord(e1, 0));
     TTS_HIP_CHECK(hipEventSynchronize(e1));
@@ -647,7 +647,7 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   std::sort(ms.begin(), ms.end());
   restore();
   a.dbg_blk = static_cast<unsigned long long*>(dalloc(static_cast<size_t>(grid) * 16 * sizeof(unsigned long long)));
-  hipLaunchKernelGGL((dev::pfsp_front_kernel<M>), dim3(grid), dim3(dev::kBlock), 0, 0, a, 0);
+  hipLaunchKernelGGL((dev::pfsp_front_kernel<M, NJ>), dim3(grid), dim3(dev::kBlock), 0, 0, a, 0);
   TTS_HIP_CHECK(hipGetLastError());
   TTS_HIP_CHECK(hipDeviceSynchronize());
   std::vector<unsigned long long> blk(static_cast<size_t>(grid) * 16);
@@ -674,11 +674,12 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
 
 // Bounds of permutation-layout parents through the front kernel (tests): parents are
 // converted on the host, bounds come back in the permutation's child order k = depth..N-1.
-template <int M>
-std::vector<int> pfsp_front_bounds_t(const PfspInstance& in, const PfspNode<20>* ph, size_t n, int device) {
-  using FNode = PfspFrontNode<M>;
+template <int M, int NJ = 20>
+std::vector<int> pfsp_front_bounds_t(const PfspInstance& in, const PfspNode<NJ>* ph, size_t n, int device) {
+  using FNode = PfspFrontNode<M, NJ>;
+  using Mask = typename FNode::Mask;
   TTS_HIP_CHECK(hipSetDevice(device));
-  const PfspFrontProblem<M> prob(in, 1);
+  const PfspFrontProblem<M, NJ> prob(in, 1);
   std::vector<FNode> fn(n);
   std::vector<int> offsets(n + 1, 0);
   for (size_t i = 0; i < n; ++i) {
@@ -688,7 +689,7 @@ std::vector<int> pfsp_front_bounds_t(const PfspInstance& in, const PfspNode<20>*
   const size_t nb = static_cast<size_t>(offsets[n]);
   std::vector<int> by_job(nb, 0), out(nb, 0);
   if (n == 0) return out;
-  dev::PfspFrontArgs<M> a{};
+  dev::PfspFrontArgs<M, NJ> a{};
   const std::vector<uint16_t> ptab = pfsp_front_fill_args(in, a);
   a.ptab = upload_vec(ptab);
   a.offsets = upload_vec(offsets);
@@ -698,7 +699,7 @@ std::vector<int> pfsp_front_bounds_t(const PfspInstance& in, const PfspNode<20>*
   a.bounds_out = dbounds;
   a.nparents = static_cast<int>(n);
   const int blocks = static_cast<int>(std::min<size_t>((n + dev::kBlock - 1) / dev::kBlock, 2048));
-  hipLaunchKernelGGL((dev::pfsp_front_bounds_kernel<M>), dim3(blocks), dim3(dev::kBlock), 0, 0, a);
+  hipLaunchKernelGGL((dev::pfsp_front_bounds_kernel<M, NJ>), dim3(blocks), dim3(dev::kBlock), 0, 0, a);
   TTS_HIP_CHECK(hipGetLastError());
   TTS_HIP_CHECK(hipDeviceSynchronize());
   TTS_HIP_CHECK(hipMemcpy(by_job.data(), dbounds, nb * sizeof(int), hipMemcpyDeviceToHost));
@@ -710,7 +711,8 @@ std::vector<int> pfsp_front_bounds_t(const PfspInstance& in, const PfspNode<20>*
     const int d = ph[i].depth;
     for (int k = d; k < in.jobs; ++k) {
       const int job = ph[i].prmu[k];
-      out[offsets[i] + (k - d)] = by_job[offsets[i] + __builtin_popcount(fn[i].rest & ((1u << job) - 1u))];
+      out[offsets[i] + (k - d)] =
+          by_job[offsets[i] + __builtin_popcountll(static_cast<unsigned long long>(fn[i].rest & ((Mask(1) << job) - 1)))];
     }
   }
   return out;
@@ -733,10 +735,16 @@ std::vector<int> pfsp_expand_probe(const PfspInstance& in, int lb, const void* p
                                    int variant, int reps = 0, std::vector<double>* timing = nullptr);
 std::vector<double> pfsp_front_time(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
                                     const EngineConfig& cfg, int reps);
-// front-layout instances only (pfsp_front_ok), defined with the 20-job bucket
+// front-layout instances only (pfsp_front_ok), defined with the 20-job bucket (the
+// 50-job front bucket's in its own TU)
 FrontProbeResult pfsp_front_probe(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
                                   const EngineConfig& cfg, unsigned cap, int split_rank = 0, int split_world = 1,
                                   size_t split_min = 0);
+FrontProbeResult pfsp_front_probe_nj50(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
+                                       const EngineConfig& cfg, unsigned cap, int split_rank, int split_world,
+                                       size_t split_min);
+std::vector<double> pfsp_front_time_nj50(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
+                                         const EngineConfig& cfg, int reps);
 
 #define TTS_PFSP_DECLARE_BUCKET(NJ)                                                                   \
   std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg); \
@@ -756,8 +764,8 @@ TTS_PFSP_DECLARE_BUCKET(500)
   std::unique_ptr<IEngine> make_pfsp_engine_nj##NJ(const PfspInstance& in, int lb, const EngineConfig& cfg) { \
     return with_machine_bucket(in.machines, [&](auto mm) -> std::unique_ptr<IEngine> {               \
       constexpr int M = decltype(mm)::value;                                                         \
-      if constexpr (NJ == 20)                                                                        \
-        if (pfsp_front_ok(in, lb)) return make_pfsp_front_engine_t<M>(in, cfg);                      \
+      if constexpr (NJ == 20 || NJ == 50)                                                            \
+        if (pfsp_front_ok(in, lb)) return make_pfsp_front_engine_t<M, NJ>(in, cfg);                  \
       if (lb != 2) return make_pfsp_engine_t<NJ, M, 1>(in, cfg);                                    \
       if (M >= 10 && lb2_pk_wanted(in)) return make_pfsp_engine_t<NJ, M, 5>(in, cfg);                 \
       return make_pfsp_engine_t<NJ, M, 2>(in, cfg);                                                  \
@@ -767,9 +775,9 @@ TTS_PFSP_DECLARE_BUCKET(500)
                                           int device) {                                              \
     return with_machine_bucket(in.machines, [&](auto mm) {                                           \
       constexpr int M = decltype(mm)::value;                                                         \
-      if constexpr (NJ == 20)                                                                        \
+      if constexpr (NJ == 20 || NJ == 50)                                                            \
         if (pfsp_front_ok(in, lb))                                                                   \
-          return pfsp_front_bounds_t<M>(in, static_cast<const PfspNode<20>*>(parents), n, device);   \
+          return pfsp_front_bounds_t<M, NJ>(in, static_cast<const PfspNode<NJ>*>(parents), n, device); \
       return lb == 2 ? pfsp_gpu_bounds_t<NJ, M, 2>(in, parents, n, best, device)                    \
                      : pfsp_gpu_bounds_t<NJ, M, 1>(in, parents, n, best, device);                   \
     });                                                                                              \

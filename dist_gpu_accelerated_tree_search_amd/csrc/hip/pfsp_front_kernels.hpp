@@ -29,10 +29,13 @@
 namespace tts {
 namespace dev {
 
-template <int M>
+template <int M, int NJ_ = 20>
 struct FrontGeom {
-  using Node = PfspFrontNode<M>;
-  static constexpr int NJ = 20;                         // at most 20 children per parent (20-job bucket)
+  static constexpr int NJ = NJ_;                        // children per parent at most (job bucket 20 or 50)
+  using Node = PfspFrontNode<M, NJ>;
+  using Mask = typename Node::Mask;                     // unscheduled-job set: 32 or 64 bits
+  static constexpr int MO = sizeof(Mask) / 4;           // first word of the set (1 or 2)
+  static constexpr int FO = 2 * MO;                     // first word of the fronts (2 or 4)
   static constexpr int NW = sizeof(Node) / 4;           // node words in registers (8 or 12)
   static constexpr int VPN = sizeof(Node) / 16;         // 16-B vectors per node
   static constexpr int BP = 256;                        // parents per chunk: one per thread
@@ -59,7 +62,8 @@ struct FrontGeom {
   // 800 / (ceil(sgpr / 16) * 16 + 16) waves), so the engine's grid uses this instead
   // (measured: a grid of 7 per CU with 6 resident made 256 workgroups start one workgroup
   // lifetime late, +1.3 us per wide iteration, +4 us per multi-level one)
-  static constexpr int WAVES = M <= 10 ? 6 : 4;
+  // (50-job nodes: 16 words for 20 machines, 12 for 10: 5 waves up to 10 machines)
+  static constexpr int WAVES = NJ > 20 ? (M <= 5 ? 6 : M <= 10 ? 5 : 4) : (M <= 10 ? 6 : 4);
   // probe records (tests): {job | kind << 8, lb, parent words, parent remain}
   static constexpr int DBGW = (2 + NW + (M + 1) / 2 + 3) / 4 * 4;
   static constexpr int HW = (M + 1) / 2;  // packed u16 pairs of a p row / a remain
@@ -68,15 +72,15 @@ struct FrontGeom {
   static constexpr int RV = (M + 7) / 8;                // 16-B vectors holding one row's M values
 };
 
-template <int M>
+template <int M, int NJ = 20>
 struct PfspFrontArgs {
-  PoolArgs<PfspFrontNode<M>> pool;
+  PoolArgs<PfspFrontNode<M, NJ>> pool;
   const uint16_t* ptab;  // job-major p, [jobs][MS], padded machines 0
   int jobs;
   int min_tails[M];      // padded machines: 0
   // bounds kernel only (tests): bounds of parent i's children at bounds_out[offsets[i] + rank of
   // the job among the parent's unscheduled jobs]
-  const PfspFrontNode<M>* parents_in;
+  const PfspFrontNode<M, NJ>* parents_in;
   const int* offsets;
   int* bounds_out;
   int nparents;
@@ -106,9 +110,9 @@ __device__ inline void front_stamp(const A& a, int k) {
   }
 }
 
-template <int M>
+template <int M, int NJ = 20>
 struct FrontSmem {
-  using G = FrontGeom<M>;
+  using G = FrontGeom<M, NJ>;
   uint16_t ptab[G::NJ][G::MS];
   int scan[kBlock / kWave];
   // dynamic local DFS (front_dyn): the workgroup's protocol state, in LDS so the step's
@@ -138,11 +142,11 @@ struct FrontSmem {
   PoolSmem<G::MAXCHUNKS> pool;
 };
 
-template <int M>
+template <int M, int NJ>
 __device__ inline void front_row(const uint16_t* row, int (&pr)[M]) {
   const uint4* r4 = reinterpret_cast<const uint4*>(row);
 #pragma unroll
-  for (int q = 0; q < FrontGeom<M>::RV; ++q) {
+  for (int q = 0; q < FrontGeom<M, NJ>::RV; ++q) {
     const uint4 x = r4[q];
     const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -151,16 +155,27 @@ __device__ inline void front_row(const uint16_t* row, int (&pr)[M]) {
   }
 }
 
-template <int M>
-__device__ inline int front_of(const uint32_t (&w)[FrontGeom<M>::NW], int m) {
-  return static_cast<int>((w[2 + (m >> 1)] >> ((m & 1) * 16)) & 0xffffu);
+template <int M, int NJ>
+__device__ inline int front_of(const uint32_t (&w)[FrontGeom<M, NJ>::NW], int m) {
+  return static_cast<int>((w[FrontGeom<M, NJ>::FO + (m >> 1)] >> ((m & 1) * 16)) & 0xffffu);
 }
 
-template <int M>
-__device__ inline void front_load(const PfspFrontNode<M>* src, uint32_t (&w)[FrontGeom<M>::NW]) {
+// The unscheduled-job set of the node held in w (word 1, or words 2-3 for 50 jobs).
+template <int M, int NJ>
+__device__ inline typename FrontGeom<M, NJ>::Mask front_mask(const uint32_t (&w)[FrontGeom<M, NJ>::NW]) {
+  if constexpr (FrontGeom<M, NJ>::MO == 1)
+    return w[1];
+  else
+    return static_cast<u64>(w[2]) | (static_cast<u64>(w[3]) << 32);
+}
+__device__ inline int mask_pop(uint32_t x) { return __popc(x); }
+__device__ inline int mask_pop(uint64_t x) { return __popcll(x); }
+
+template <int M, int NJ>
+__device__ inline void front_load(const PfspFrontNode<M, NJ>* src, uint32_t (&w)[FrontGeom<M, NJ>::NW]) {
   const uint4* s = reinterpret_cast<const uint4*>(src);
 #pragma unroll
-  for (int q = 0; q < FrontGeom<M>::VPN; ++q) {
+  for (int q = 0; q < FrontGeom<M, NJ>::VPN; ++q) {
     const uint4 x = s[q];
     w[4 * q] = x.x;
     w[4 * q + 1] = x.y;
@@ -169,20 +184,20 @@ __device__ inline void front_load(const PfspFrontNode<M>* src, uint32_t (&w)[Fro
   }
 }
 
-template <int M>
-__device__ inline void front_store(uint4* dst, const uint32_t (&c)[FrontGeom<M>::NW]) {
+template <int M, int NJ>
+__device__ inline void front_store(uint4* dst, const uint32_t (&c)[FrontGeom<M, NJ>::NW]) {
 #pragma unroll
-  for (int q = 0; q < FrontGeom<M>::VPN; ++q) dst[q] = make_uint4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
+  for (int q = 0; q < FrontGeom<M, NJ>::VPN; ++q) dst[q] = make_uint4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
 }
 
 // Probe record of one evaluated child (tests; a.dbg_rec is null in production): the
 // parent's words, its remain (packed u16 pairs, tails excluded), the job, the iteration
 // shape (kind) and the bound. The host recomputes every field (pfsp_front_probe).
 enum FrontDbgKind { kDbgOne = 0, kDbgCp = 1, kDbgTp = 2, kDbgLocal = 3, kDbgSplit = 4, kDbgDyn = 5 };
-template <int M>
-__device__ inline void front_dbg(const PfspFrontArgs<M>& a, int kind, const uint32_t (&w)[FrontGeom<M>::NW],
-                                 const uint32_t (&rp)[FrontGeom<M>::HW], int j, int lb) {
-  using G = FrontGeom<M>;
+template <int M, int NJ>
+__device__ inline void front_dbg(const PfspFrontArgs<M, NJ>& a, int kind, const uint32_t (&w)[FrontGeom<M, NJ>::NW],
+                                 const uint32_t (&rp)[FrontGeom<M, NJ>::HW], int j, int lb) {
+  using G = FrontGeom<M, NJ>;
   const unsigned i = atomicAdd(a.dbg_n, 1u);
   if (i >= a.dbg_cap) return;
   uint32_t* r = a.dbg_rec + static_cast<size_t>(i) * G::DBGW;
@@ -202,18 +217,18 @@ __device__ inline void front_dbg(const PfspFrontArgs<M>& a, int kind, const uint
 // Bounds of the children appending the jobs of `rest` to a parent whose front / remain +
 // tail are fb[m] / rb[m] (each value in both halves): emit(j, lb) per job, ascending,
 // two jobs per pass (ref add_front_and_bound, c_bound_simple.c:219-244).
-template <int M, class Emit>
-__device__ inline void front_bounds_x2(const FrontSmem<M>& sm, const uint32_t (&fb)[M], const uint32_t (&rb)[M],
-                                       uint32_t rest, Emit emit) {
-  constexpr int HW = FrontGeom<M>::HW;
+template <int M, int NJ, class Emit>
+__device__ inline void front_bounds_x2(const FrontSmem<M, NJ>& sm, const uint32_t (&fb)[M], const uint32_t (&rb)[M],
+                                       typename FrontGeom<M, NJ>::Mask rest, Emit emit) {
+  constexpr int HW = FrontGeom<M, NJ>::HW;
   // 20 machines: one child per pass (same-box A/B on ta021 LB1_d: packed pairs 9.82 s,
   // one child 9.31 s; on ta014's 10 machines the pairs win, 0.2245 -> 0.2209 ms:
   // profiles/r4/packed_bounds_ab.txt)
   if constexpr (M > 10) {
-    for (uint32_t x = rest; x; x &= x - 1) {
-      const int j = __builtin_ctz(x);
+    for (auto x = rest; x; x &= x - 1) {
+      const int j = mask_ctz(x);
       int pr[M];
-      front_row<M>(sm.ptab[j], pr);
+      front_row<M, NJ>(sm.ptab[j], pr);
       int lb = static_cast<int>(fb[0] & 0xffffu) + static_cast<int>(rb[0] & 0xffffu);
       int tt = static_cast<int>(fb[0] & 0xffffu) + pr[0];
 #pragma unroll
@@ -226,11 +241,11 @@ __device__ inline void front_bounds_x2(const FrontSmem<M>& sm, const uint32_t (&
     }
     return;
   }
-  for (uint32_t x = rest; x;) {
-    const int j1 = __builtin_ctz(x);
+  for (auto x = rest; x;) {
+    const int j1 = mask_ctz(x);
     x &= x - 1;
     const bool two = x != 0;
-    const int j2 = two ? __builtin_ctz(x) : j1;
+    const int j2 = two ? mask_ctz(x) : j1;
     x &= x - 1;
     const uint32_t* r1 = reinterpret_cast<const uint32_t*>(sm.ptab[j1]);
     const uint32_t* r2 = reinterpret_cast<const uint32_t*>(sm.ptab[j2]);
@@ -256,101 +271,106 @@ __device__ inline void front_bounds_x2(const FrontSmem<M>& sm, const uint32_t (&
 }
 
 // fb / rb of a parent: its front (words of w) and its packed remain rp plus the tails
-template <int M>
-__device__ inline void front_broadcast(const PfspFrontArgs<M>& a, const uint32_t (&w)[FrontGeom<M>::NW],
-                                       const uint32_t (&rp)[FrontGeom<M>::HW], uint32_t (&fb)[M], uint32_t (&rb)[M]) {
+template <int M, int NJ>
+__device__ inline void front_broadcast(const PfspFrontArgs<M, NJ>& a, const uint32_t (&w)[FrontGeom<M, NJ>::NW],
+                                       const uint32_t (&rp)[FrontGeom<M, NJ>::HW], uint32_t (&fb)[M], uint32_t (&rb)[M]) {
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    fb[m] = static_cast<uint32_t>(front_of<M>(w, m)) * 0x10001u;
+    fb[m] = static_cast<uint32_t>(front_of<M, NJ>(w, m)) * 0x10001u;
     rb[m] = (((rp[m >> 1] >> ((m & 1) * 16)) & 0xffffu) + static_cast<uint32_t>(a.min_tails[m])) * 0x10001u;
   }
 }
 
 // The packed remain of the node in w: the sum of its unscheduled jobs' p rows.
-template <int M>
-__device__ inline void front_remain(const FrontSmem<M>& sm, const uint32_t (&w)[FrontGeom<M>::NW],
-                                    uint32_t (&r2)[FrontGeom<M>::HW]) {
+template <int M, int NJ>
+__device__ inline void front_remain(const FrontSmem<M, NJ>& sm, const uint32_t (&w)[FrontGeom<M, NJ>::NW],
+                                    uint32_t (&r2)[FrontGeom<M, NJ>::HW]) {
 #pragma unroll
-  for (int h = 0; h < FrontGeom<M>::HW; ++h) r2[h] = 0;
-  for (uint32_t x = w[1]; x; x &= x - 1) {
-    const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[__builtin_ctz(x)]);
+  for (int h = 0; h < FrontGeom<M, NJ>::HW; ++h) r2[h] = 0;
+  for (auto x = front_mask<M, NJ>(w); x; x &= x - 1) {
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[mask_ctz(x)]);
 #pragma unroll
-    for (int h = 0; h < FrontGeom<M>::HW; ++h) r2[h] += row[h];
+    for (int h = 0; h < FrontGeom<M, NJ>::HW; ++h) r2[h] += row[h];
   }
 }
 
 // Bounds of every child of the parent held in w: emit(j, lb) for each unscheduled job j.
 // (the parent's packed remain rp given)
-template <int M, class Emit>
-__device__ inline void front_parent_r(const PfspFrontArgs<M>& a, const FrontSmem<M>& sm,
-                                      const uint32_t (&w)[FrontGeom<M>::NW], const uint32_t (&rp)[FrontGeom<M>::HW],
+template <int M, int NJ, class Emit>
+__device__ inline void front_parent_r(const PfspFrontArgs<M, NJ>& a, const FrontSmem<M, NJ>& sm,
+                                      const uint32_t (&w)[FrontGeom<M, NJ>::NW], const uint32_t (&rp)[FrontGeom<M, NJ>::HW],
                                       Emit emit, int kind) {
   uint32_t fb[M], rb[M];
-  front_broadcast<M>(a, w, rp, fb, rb);
-  front_bounds_x2<M>(sm, fb, rb, w[1], [&](int j, int lb) {
-    if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
+  front_broadcast<M, NJ>(a, w, rp, fb, rb);
+  front_bounds_x2<M, NJ>(sm, fb, rb, front_mask<M, NJ>(w), [&](int j, int lb) {
+    if (a.dbg_rec) front_dbg<M, NJ>(a, kind, w, rp, j, lb);
     emit(j, lb);
   });
 }
 
-template <int M, class Emit>
-__device__ inline void front_parent(const PfspFrontArgs<M>& a, const FrontSmem<M>& sm,
-                                    const uint32_t (&w)[FrontGeom<M>::NW], Emit emit, int kind = kDbgOne) {
-  uint32_t rp[FrontGeom<M>::HW], fb[M], rb[M];
-  front_remain<M>(sm, w, rp);
-  front_broadcast<M>(a, w, rp, fb, rb);
-  front_bounds_x2<M>(sm, fb, rb, w[1], [&](int j, int lb) {
-    if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
+template <int M, int NJ, class Emit>
+__device__ inline void front_parent(const PfspFrontArgs<M, NJ>& a, const FrontSmem<M, NJ>& sm,
+                                    const uint32_t (&w)[FrontGeom<M, NJ>::NW], Emit emit, int kind = kDbgOne) {
+  uint32_t rp[FrontGeom<M, NJ>::HW], fb[M], rb[M];
+  front_remain<M, NJ>(sm, w, rp);
+  front_broadcast<M, NJ>(a, w, rp, fb, rb);
+  front_bounds_x2<M, NJ>(sm, fb, rb, front_mask<M, NJ>(w), [&](int j, int lb) {
+    if (a.dbg_rec) front_dbg<M, NJ>(a, kind, w, rp, j, lb);
     emit(j, lb);
   });
 }
 
 // Child of the parent in w that appends job j: depth + 1, j removed from the set, and
 // its front (the chain from the parent's front; from 0 at the root).
-template <int M>
-__device__ inline void front_child(const FrontSmem<M>& sm, const uint32_t (&w)[FrontGeom<M>::NW], int j,
-                                   uint32_t (&c)[FrontGeom<M>::NW]) {
-  constexpr int NW = FrontGeom<M>::NW;
+template <int M, int NJ>
+__device__ inline void front_child(const FrontSmem<M, NJ>& sm, const uint32_t (&w)[FrontGeom<M, NJ>::NW], int j,
+                                   uint32_t (&c)[FrontGeom<M, NJ>::NW]) {
+  constexpr int NW = FrontGeom<M, NJ>::NW;
   const int d = static_cast<int>(w[0] & 0xffu);
   const bool root = d == 0;
   int pr[M];
-  front_row<M>(sm.ptab[j], pr);
+  front_row<M, NJ>(sm.ptab[j], pr);
+  constexpr int FO = FrontGeom<M, NJ>::FO;
   c[0] = static_cast<uint32_t>(d + 1);
-  c[1] = w[1] & ~(1u << j);
 #pragma unroll
-  for (int i = 2; i < NW; ++i) c[i] = 0;
-  int ft = (root ? 0 : front_of<M>(w, 0)) + pr[0];
-  c[2] = static_cast<uint32_t>(ft);
+  for (int i = 1; i < NW; ++i) c[i] = 0;
+  const auto rest = front_mask<M, NJ>(w) & ~(static_cast<typename FrontGeom<M, NJ>::Mask>(1) << j);
+  c[FrontGeom<M, NJ>::MO] = static_cast<uint32_t>(rest);
+  if constexpr (FrontGeom<M, NJ>::MO == 2) c[3] = static_cast<uint32_t>(static_cast<u64>(rest) >> 32);
+  int ft = (root ? 0 : front_of<M, NJ>(w, 0)) + pr[0];
+  c[FO] = static_cast<uint32_t>(ft);
 #pragma unroll
   for (int m = 1; m < M; ++m) {
-    ft = max(ft, root ? 0 : front_of<M>(w, m)) + pr[m];
-    c[2 + (m >> 1)] |= static_cast<uint32_t>(ft) << ((m & 1) * 16);
+    ft = max(ft, root ? 0 : front_of<M, NJ>(w, m)) + pr[m];
+    c[FO + (m >> 1)] |= static_cast<uint32_t>(ft) << ((m & 1) * 16);
   }
 }
 
 // (store(i, child words, job) for the i-th surviving child of w)
-template <int M, class Store>
-__device__ inline void front_emit_to(const FrontSmem<M>& sm, const uint32_t (&w)[FrontGeom<M>::NW], uint32_t surv,
+template <int M, int NJ, class Store>
+__device__ inline void front_emit_to(const FrontSmem<M, NJ>& sm, const uint32_t (&w)[FrontGeom<M, NJ>::NW],
+                                     typename FrontGeom<M, NJ>::Mask surv,
                                      Store store) {
   for (int i = 0; surv; ++i) {
-    const int j = __builtin_ctz(surv);
+    const int j = mask_ctz(surv);
     surv &= surv - 1;
-    uint32_t c[FrontGeom<M>::NW];
-    front_child<M>(sm, w, j, c);
+    uint32_t c[FrontGeom<M, NJ>::NW];
+    front_child<M, NJ>(sm, w, j, c);
     store(i, c, j);
   }
 }
 
-template <int M>
-__device__ inline void front_emit(const FrontSmem<M>& sm, const uint32_t (&w)[FrontGeom<M>::NW], uint32_t surv,
+template <int M, int NJ>
+__device__ inline void front_emit(const FrontSmem<M, NJ>& sm, const uint32_t (&w)[FrontGeom<M, NJ>::NW],
+                                  typename FrontGeom<M, NJ>::Mask surv,
                                   uint4* dst) {
   while (surv) {
-    const int j = __builtin_ctz(surv);
+    const int j = mask_ctz(surv);
     surv &= surv - 1;
-    uint32_t c[FrontGeom<M>::NW];
-    front_child<M>(sm, w, j, c);
-    front_store<M>(dst, c);
-    dst += FrontGeom<M>::VPN;
+    uint32_t c[FrontGeom<M, NJ>::NW];
+    front_child<M, NJ>(sm, w, j, c);
+    front_store<M, NJ>(dst, c);
+    dst += FrontGeom<M, NJ>::VPN;
   }
 }
 
@@ -369,6 +389,12 @@ __device__ inline int kth_bit(uint32_t x, int k) {
   }
   return pos;
 }
+// (64-bit sets: the low word first)
+__device__ inline int kth_bit(uint64_t x, int k) {
+  const uint32_t lo = static_cast<uint32_t>(x);
+  const int c = __popc(lo);
+  return k < c ? kth_bit(lo, k) : 32 + kth_bit(static_cast<uint32_t>(x >> 32), k - c);
+}
 
 // Child-parallel expansion of n nodes staged in LDS (src[i], with their remain
 // rem[i]): ONE THREAD PER CHILD instead of one per parent. In a narrow level a
@@ -380,10 +406,15 @@ __device__ inline int kth_bit(uint32_t x, int k) {
 // survivors are compacted (block scan) and handed to store(index, child words, child
 // remain). Returns the survivor count. Every thread calls it (block-wide scans).
 // Children of the n staged nodes: their offsets into sm.coff, the total returned.
-template <int M>
-__device__ inline int front_child_offsets(FrontSmem<M>& sm, const uint4 (*src)[FrontGeom<M>::VPN], int n) {
+template <int M, int NJ>
+__device__ inline int front_child_offsets(FrontSmem<M, NJ>& sm, const uint4 (*src)[FrontGeom<M, NJ>::VPN], int n) {
   int T = 0;
-  const int off = block_exclusive_scan(threadIdx.x < n ? __popc(src[threadIdx.x][0].y) : 0, sm.scan, &T);
+  int k = 0;
+  if (static_cast<int>(threadIdx.x) < n) {
+    const uint4 h = src[threadIdx.x][0];  // the set: word 1 (20 jobs) or words 2-3 (50 jobs)
+    k = FrontGeom<M, NJ>::MO == 1 ? __popc(h.y) : __popc(h.z) + __popc(h.w);
+  }
+  const int off = block_exclusive_scan(k, sm.scan, &T);
   if (static_cast<int>(threadIdx.x) < n) sm.coff[threadIdx.x] = off;
   __syncthreads();
   return T;
@@ -395,11 +426,11 @@ struct FrontKeepAll {
 };
 
 // (T children, offsets in sm.coff: front_child_offsets)
-template <int M, class Store, class Keep = FrontKeepAll>
-__device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const uint4 (*src)[FrontGeom<M>::VPN],
-                                      const uint32_t (*rem)[FrontGeom<M>::HW], int n, int T, int best, int& nleaf,
+template <int M, int NJ, class Store, class Keep = FrontKeepAll>
+__device__ inline int front_expand_cp(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>& sm, const uint4 (*src)[FrontGeom<M, NJ>::VPN],
+                                      const uint32_t (*rem)[FrontGeom<M, NJ>::HW], int n, int T, int best, int& nleaf,
                                       Store store, Keep keep = {}, int kind = kDbgCp) {
-  using G = FrontGeom<M>;
+  using G = FrontGeom<M, NJ>;
   constexpr int HW = G::HW;
   const int tid = threadIdx.x;
   int nout = 0;
@@ -429,7 +460,7 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
         w[4 * q + 2] = x.z;
         w[4 * q + 3] = x.w;
       }
-      j = kth_bit(w[1], c - sm.coff[lo]);
+      j = kth_bit(front_mask<M, NJ>(w), c - sm.coff[lo]);
       const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
       uint32_t pw[HW], rp[HW];
 #pragma unroll
@@ -440,16 +471,16 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
       }
       auto pm = [&](int m) { return static_cast<int>((pw[m >> 1] >> ((m & 1) * 16)) & 0xffffu); };
       auto rm = [&](int m) { return static_cast<int>((rp[m >> 1] >> ((m & 1) * 16)) & 0xffffu) + a.min_tails[m]; };
-      const int f0 = front_of<M>(w, 0);
+      const int f0 = front_of<M, NJ>(w, 0);
       int lb = f0 + rm(0);
       int tt = f0 + pm(0);
 #pragma unroll
       for (int m = 1; m < M; ++m) {
-        const int sv = max(tt, front_of<M>(w, m));
+        const int sv = max(tt, front_of<M, NJ>(w, m));
         lb = max(lb, sv + rm(m));
         tt = sv + pm(m);
       }
-      if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
+      if (a.dbg_rec) front_dbg<M, NJ>(a, kind, w, rp, j, lb);
       const bool kp = keep(lo, j);
       if (static_cast<int>(w[0] & 0xffu) + 1 == a.jobs) {
         nleaf += kp;
@@ -462,7 +493,7 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
     const int idx = nout + block_exclusive_scan(surv ? 1 : 0, sm.scan, &tot);
     if (surv) {
       uint32_t cw[G::NW];
-      front_child<M>(sm, w, j, cw);
+      front_child<M, NJ>(sm, w, j, cw);
       store(idx, cw, cr);
     }
     nout += tot;
@@ -477,37 +508,37 @@ __device__ inline int front_expand_cp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
 // path: fewer instructions per child than front_expand_cp (no parent search, one node
 // load per parent), and the serial loop is short once most lanes hold a node.
 // (the node and its packed remain in registers; w = 0 for a thread without a node)
-template <int M, class Store, class Keep = FrontKeepAll>
-__device__ inline int front_expand_tp_regs(const PfspFrontArgs<M>& a, FrontSmem<M>& sm,
-                                           const uint32_t (&w)[FrontGeom<M>::NW], const uint32_t (&rp)[FrontGeom<M>::HW],
+template <int M, int NJ, class Store, class Keep = FrontKeepAll>
+__device__ inline int front_expand_tp_regs(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>& sm,
+                                           const uint32_t (&w)[FrontGeom<M, NJ>::NW], const uint32_t (&rp)[FrontGeom<M, NJ>::HW],
                                            int best, int& nleaf, Store store, int kind = kDbgTp, Keep keep = {}) {
-  using G = FrontGeom<M>;
+  using G = FrontGeom<M, NJ>;
   constexpr int HW = G::HW;
-  uint32_t surv = 0;
+  typename G::Mask surv = 0;
   int nsurv = 0;
   const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
   {
     uint32_t fb[M], rb[M];
-    front_broadcast<M>(a, w, rp, fb, rb);
-    front_bounds_x2<M>(sm, fb, rb, w[1], [&](int j, int lb) {
-      if (a.dbg_rec) front_dbg<M>(a, kind, w, rp, j, lb);
+    front_broadcast<M, NJ>(a, w, rp, fb, rb);
+    front_bounds_x2<M, NJ>(sm, fb, rb, front_mask<M, NJ>(w), [&](int j, int lb) {
+      if (a.dbg_rec) front_dbg<M, NJ>(a, kind, w, rp, j, lb);
       const bool kp = keep(static_cast<int>(threadIdx.x), j);
       if (leaf) {
         nleaf += kp;
         if (lb < best) atomicMin(&a.pool.ctl->best.v, lb);
       } else if (kp && lb < best) {
         ++nsurv;
-        surv |= 1u << j;
+        surv |= static_cast<typename G::Mask>(1) << j;
       }
     });
   }
   int tot = 0;
   int idx = block_exclusive_scan(nsurv, sm.scan, &tot);
   while (surv) {
-    const int j = __builtin_ctz(surv);
+    const int j = mask_ctz(surv);
     surv &= surv - 1;
     uint32_t cw[G::NW], cr[HW];
-    front_child<M>(sm, w, j, cw);
+    front_child<M, NJ>(sm, w, j, cw);
     const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
 #pragma unroll
     for (int h = 0; h < HW; ++h) cr[h] = rp[h] - row[h];
@@ -516,11 +547,11 @@ __device__ inline int front_expand_tp_regs(const PfspFrontArgs<M>& a, FrontSmem<
   return tot;
 }
 
-template <int M, class Store, class Keep = FrontKeepAll>
-__device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& sm,
-                                      const uint4 (*src)[FrontGeom<M>::VPN], const uint32_t (*rem)[FrontGeom<M>::HW],
+template <int M, int NJ, class Store, class Keep = FrontKeepAll>
+__device__ inline int front_expand_tp(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>& sm,
+                                      const uint4 (*src)[FrontGeom<M, NJ>::VPN], const uint32_t (*rem)[FrontGeom<M, NJ>::HW],
                                       int n, int best, int& nleaf, Store store, Keep keep = {}, int kind = kDbgTp) {
-  using G = FrontGeom<M>;
+  using G = FrontGeom<M, NJ>;
   constexpr int HW = G::HW;
   const int tid = threadIdx.x;
   uint32_t w[G::NW], rp[HW];
@@ -540,7 +571,7 @@ __device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
 #pragma unroll
     for (int h = 0; h < HW; ++h) rp[h] = rem[tid][h];
   }
-  return front_expand_tp_regs<M>(a, sm, w, rp, best, nleaf, store, kind, keep);
+  return front_expand_tp_regs<M, NJ>(a, sm, w, rp, best, nleaf, store, kind, keep);
 }
 
 // Multi-level chunk (fused iterations): the chunk's v.bp parents go to LDS with their
@@ -552,11 +583,11 @@ __device__ inline int front_expand_tp(const PfspFrontArgs<M>& a, FrontSmem<M>& s
 // nodes (high half of the leaf word); everything that goes out is the chunk's output.
 // One dependent kernel covers up to 4 tree levels of a narrow window (ref: one kernel
 // per level, pfsp_multigpu_cuda.c:221-332).
-template <int M>
-__device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t,
+template <int M, int NJ>
+__device__ inline void front_multi_level(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>& sm, const IterView& v, int t,
                                          int best) {
-  using G = FrontGeom<M>;
-  using Node = PfspFrontNode<M>;
+  using G = FrontGeom<M, NJ>;
+  using Node = PfspFrontNode<M, NJ>;
   static_assert(G::BPF_CP * (G::NJ - 1) + (G::LMAX - 1) * G::CAP * (G::NJ - 1) <= G::SLOT,
                 "chunk output must fit its slot region");
   static_assert(kBlock * (G::NJ - 1) + (G::WLMAX - 1) * G::CAP * (G::NJ - 1) <= G::SLOT,
@@ -581,22 +612,22 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
       uint32_t w[G::NW], r2[G::HW];
 #pragma unroll
       for (int i = 0; i < G::NW; ++i) w[i] = 0;
-      if (tid < n0) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
-      front_remain<M>(sm, w, r2);
+      if (tid < n0) front_load<M, NJ>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
+      front_remain<M, NJ>(sm, w, r2);
       const bool last = L == 1;
       // the first LDS level: both buffers when it is also the last one expanded (two
       // levels), else buffer 1 (buffer 0 then takes the level after it)
       const int cap1 = L == 2 ? 2 * G::CAP : G::CAP;
       const int base1 = L == 2 ? 0 : G::CAP;
-      const int nn = front_expand_tp_regs<M>(
+      const int nn = front_expand_tp_regs<M, NJ>(
           a, sm, w, r2, best, nleaf,
           [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {
             if (!last && i < cap1) {
-              front_store<M>(&sm.lvl[base1 + i][0], c);
+              front_store<M, NJ>(&sm.lvl[base1 + i][0], c);
 #pragma unroll
               for (int h = 0; h < G::HW; ++h) sm.rlv[base1 + i][h] = r[h];
             } else {
-              front_store<M>(out + (last ? i : i - cap1) * G::VPN, c);
+              front_store<M, NJ>(out + (last ? i : i - cap1) * G::VPN, c);
             }
           },
           kDbgOne);
@@ -612,9 +643,9 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
         // the parent's remain: one pass over its unscheduled rows (packed u16 pairs; sums
         // < 65536, pfsp_front_ok), by the thread that stages it
         uint32_t w[G::NW], r2[G::HW];
-        front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
-        front_store<M>(&sm.lvl[tid][0], w);
-        front_remain<M>(sm, w, r2);
+        front_load<M, NJ>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, g0 + tid, sm.pool), w);
+        front_store<M, NJ>(&sm.lvl[tid][0], w);
+        front_remain<M, NJ>(sm, w, r2);
 #pragma unroll
         for (int h = 0; h < G::HW; ++h) sm.rlv[tid][h] = r2[h];
       }
@@ -626,24 +657,24 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
       const int nx = cur ^ 1;
       auto store = [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {
         if (!last && i < G::CAP) {
-          front_store<M>(&sm.lvl[nx * G::CAP + i][0], c);
+          front_store<M, NJ>(&sm.lvl[nx * G::CAP + i][0], c);
 #pragma unroll
           for (int h = 0; h < G::HW; ++h) sm.rlv[nx * G::CAP + i][h] = r[h];
         } else {
-          front_store<M>(out + (o + (last ? i : i - G::CAP)) * G::VPN, c);
+          front_store<M, NJ>(out + (o + (last ? i : i - G::CAP)) * G::VPN, c);
         }
       };
       const uint4(*src)[G::VPN] = sm.lvl + cur * G::CAP;
       const uint32_t(*rsrc)[G::HW] = sm.rlv + cur * G::CAP;
-      const int T = front_child_offsets<M>(sm, src, n);
+      const int T = front_child_offsets<M, NJ>(sm, src, n);
       // the first level of a rank split's iteration keeps this rank's children only
       // (split_keep of the parent's window position and the job, as the one-level split)
       const bool split_lev = v.split && lev == 0;
       const u64 gbase = g0;
       auto keep = [&](int p, int j) { return !split_lev || split_keep(v, gbase + static_cast<u64>(p), j); };
       const int nn = T > a.cp_max
-                         ? front_expand_tp<M>(a, sm, src, rsrc, n, best, nleaf, store, keep, split_lev ? kDbgSplit : kDbgTp)
-                         : front_expand_cp<M>(a, sm, src, rsrc, n, T, best, nleaf, store, keep,
+                         ? front_expand_tp<M, NJ>(a, sm, src, rsrc, n, best, nleaf, store, keep, split_lev ? kDbgSplit : kDbgTp)
+                         : front_expand_cp<M, NJ>(a, sm, src, rsrc, n, T, best, nleaf, store, keep,
                                               split_lev ? kDbgSplit : kDbgCp);
       __syncthreads();  // the next level is visible; this level's buffer is free
       o += last ? nn : max(0, nn - G::CAP);
@@ -671,10 +702,10 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M>& a, FrontSmem<M>
 // (cnt); nodes pushed and expanded in between are explored tree nodes (high half of
 // the leaf word). Pops read slots [top - n, top) and pushes write from top - n on:
 // every pop is in registers before the scan's barrier that precedes the first push.
-template <int M>
-__device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t, int best) {
-  using G = FrontGeom<M>;
-  using Node = PfspFrontNode<M>;
+template <int M, int NJ>
+__device__ inline void front_local(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>& sm, const IterView& v, int t, int best) {
+  using G = FrontGeom<M, NJ>;
+  using Node = PfspFrontNode<M, NJ>;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   Node* const bout = pa.buf[(t & 1) ^ 1];
@@ -693,7 +724,7 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
       if (s == 0) {
         const u64 gi = v.stride ? static_cast<u64>(ch) + static_cast<u64>(tid) * static_cast<u64>(v.nchunks)
                                        : static_cast<u64>(ch) * v.bp + tid;
-        if (tid < v.bp && gi < v.B) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
+        if (tid < v.bp && gi < v.B) front_load<M, NJ>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
       } else {
         if (top == 0) break;  // uniform
         const int npop = min(top, kBlock);
@@ -712,16 +743,16 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
             for (int h = 0; h < G::HW; ++h) rp[h] = sm.stage_r[k][h];
             have_r = true;
           } else {
-            front_load<M>(stk + (top - npop + tid), w);
+            front_load<M, NJ>(stk + (top - npop + tid), w);
           }
         }
         top -= npop;
       }
-      uint32_t surv = 0;
+      typename G::Mask surv = 0;
       int nsurv = 0;
       const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-      if (!have_r) front_remain<M>(sm, w, rp);
-      front_parent_r<M>(
+      if (!have_r) front_remain<M, NJ>(sm, w, rp);
+      front_parent_r<M, NJ>(
           a, sm, w, rp,
           [&](int j, int lb) {
             if (leaf) {
@@ -729,7 +760,7 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
               if (lb < best) atomicMin(&pa.ctl->best.v, lb);
             } else if (lb < best) {
               ++nsurv;
-              surv |= 1u << j;
+              surv |= static_cast<typename G::Mask>(1) << j;
             }
           },
           kDbgLocal);
@@ -743,15 +774,15 @@ __device__ inline void front_local(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, 
       const int lo = tot - nst;
       uint4* const dst = reinterpret_cast<uint4*>(stk + top);
       // (the scan's barrier: every thread holds its popped node in registers by now)
-      front_emit_to<M>(sm, w, surv, [&](int i, const uint32_t (&c)[G::NW], int j) {
+      front_emit_to<M, NJ>(sm, w, surv, [&](int i, const uint32_t (&c)[G::NW], int j) {
         const int o = off + i;
         if (o >= lo) {
-          front_store<M>(&sm.stage[o - lo][0], c);
+          front_store<M, NJ>(&sm.stage[o - lo][0], c);
           const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
 #pragma unroll
           for (int h = 0; h < G::HW; ++h) sm.stage_r[o - lo][h] = rp[h] - row[h];  // the child's remain
         } else {
-          front_store<M>(dst + o * G::VPN, c);
+          front_store<M, NJ>(dst + o * G::VPN, c);
         }
       });
       top = tnew;
@@ -808,19 +839,19 @@ __device__ inline bool dyn_cas(unsigned* p, unsigned expect, unsigned want) {
                                               __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int M>
-__device__ inline void dyn_node_store(PfspFrontNode<M>* dst, const uint32_t (&w)[FrontGeom<M>::NW]) {
+template <int M, int NJ>
+__device__ inline void dyn_node_store(PfspFrontNode<M, NJ>* dst, const uint32_t (&w)[FrontGeom<M, NJ>::NW]) {
   u64* d = reinterpret_cast<u64*>(dst);
 #pragma unroll
-  for (int k = 0; k < FrontGeom<M>::NW / 2; ++k)
+  for (int k = 0; k < FrontGeom<M, NJ>::NW / 2; ++k)
     __hip_atomic_store(d + k, static_cast<u64>(w[2 * k]) | (static_cast<u64>(w[2 * k + 1]) << 32), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
-template <int M>
-__device__ inline void dyn_node_load(PfspFrontNode<M>* src, uint32_t (&w)[FrontGeom<M>::NW]) {
+template <int M, int NJ>
+__device__ inline void dyn_node_load(PfspFrontNode<M, NJ>* src, uint32_t (&w)[FrontGeom<M, NJ>::NW]) {
   u64* s = reinterpret_cast<u64*>(src);
 #pragma unroll
-  for (int k = 0; k < FrontGeom<M>::NW / 2; ++k) {
+  for (int k = 0; k < FrontGeom<M, NJ>::NW / 2; ++k) {
     const u64 x = __hip_atomic_load(s + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     w[2 * k] = static_cast<uint32_t>(x);
     w[2 * k + 1] = static_cast<uint32_t>(x >> 32);
@@ -852,10 +883,10 @@ __device__ inline int dyn_take(DynCtl* dc, int qbase, int qx, unsigned want, uns
   return -1;
 }
 
-template <int M>
-__device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, const IterView& v, int t, int best0) {
-  using G = FrontGeom<M>;
-  using Node = PfspFrontNode<M>;
+template <int M, int NJ>
+__device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>& sm, const IterView& v, int t, int best0) {
+  using G = FrontGeom<M, NJ>;
+  using Node = PfspFrontNode<M, NJ>;
   constexpr int NW = G::NW;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
@@ -887,9 +918,9 @@ __device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, co
     const int claim = s == 0 ? -1 : sm.dyn.claim;
     if (s == 0) {
       const u64 gi = static_cast<u64>(ch) + static_cast<u64>(tid) * static_cast<u64>(v.nchunks);
-      if (tid < v.bp && gi < v.B) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
+      if (tid < v.bp && gi < v.B) front_load<M, NJ>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
     } else if (claim >= 0) {
-      if (tid < sm.dyn.claim_n) dyn_node_load<M>(region(claim) + tid, w);
+      if (tid < sm.dyn.claim_n) dyn_node_load<M, NJ>(region(claim) + tid, w);
     } else {
       const int npop = min(top, kBlock);
       if (tid < npop) {
@@ -907,17 +938,17 @@ __device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, co
           for (int h = 0; h < G::HW; ++h) rp[h] = sm.stage_r[k][h];
           have_r = true;
         } else {
-          front_load<M>(stk + (top - npop + tid), w);
+          front_load<M, NJ>(stk + (top - npop + tid), w);
         }
       }
       top -= npop;
       if (tid == 0) sm.dyn.inner += npop;
     }
-    uint32_t surv = 0;
+    typename G::Mask surv = 0;
     int nsurv = 0;
     const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
-    if (!have_r) front_remain<M>(sm, w, rp);
-    front_parent_r<M>(
+    if (!have_r) front_remain<M, NJ>(sm, w, rp);
+    front_parent_r<M, NJ>(
         a, sm, w, rp,
         [&](int j, int lb) {
           if (leaf) {
@@ -925,7 +956,7 @@ __device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, co
             if (lb < best) atomicMin(&pa.ctl->best.v, lb);
           } else if (lb < best) {
             ++nsurv;
-            surv |= 1u << j;
+            surv |= static_cast<typename G::Mask>(1) << j;
           }
         },
         kDbgDyn);
@@ -936,15 +967,15 @@ __device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, co
     nst = min(tot, min(tnew, kBlock));  // the next pop stays in LDS
     const int lo = tot - nst;
     uint4* const dst = reinterpret_cast<uint4*>(stk + top);
-    front_emit_to<M>(sm, w, surv, [&](int i, const uint32_t (&c)[NW], int j) {
+    front_emit_to<M, NJ>(sm, w, surv, [&](int i, const uint32_t (&c)[NW], int j) {
       const int o = off + i;
       if (o >= lo) {
-        front_store<M>(&sm.stage[o - lo][0], c);
+        front_store<M, NJ>(&sm.stage[o - lo][0], c);
         const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j]);
 #pragma unroll
         for (int h = 0; h < G::HW; ++h) sm.stage_r[o - lo][h] = rp[h] - row[h];
       } else {
-        front_store<M>(dst + o * G::VPN, c);
+        front_store<M, NJ>(dst + o * G::VPN, c);
       }
     });
     top = tnew;
@@ -995,9 +1026,9 @@ __device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, co
             x[4 * q + 3] = y.w;
           }
         } else {
-          front_load<M>(stk + (top - n + tid), x);
+          front_load<M, NJ>(stk + (top - n + tid), x);
         }
-        dyn_node_store<M>(region(sm.dyn.dslot) + tid, x);
+        dyn_node_store<M, NJ>(region(sm.dyn.dslot) + tid, x);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload is complete
       __syncthreads();
@@ -1052,7 +1083,7 @@ __device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, co
       x[4 * q + 2] = y.z;
       x[4 * q + 3] = y.w;
     }
-    front_store<M>(reinterpret_cast<uint4*>(stk + (top - nst + tid)), x);
+    front_store<M, NJ>(reinterpret_cast<uint4*>(stk + (top - nst + tid)), x);
   }
   int leaves = 0;
   (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
@@ -1098,12 +1129,12 @@ __device__ inline void front_dyn(const PfspFrontArgs<M>& a, FrontSmem<M>& sm, co
 // 4 for 20 (f, remain and a p row stay in registers without scratch); FrontGeom::WAVES
 // sizes the engine's grid to match. (Compiled for 7 — 94 SGPRs, 72 spilled to VGPR
 // lanes — the headline was 3 % slower than at 6.)
-template <int M>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FrontGeom<M>::WAVES)))
-void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
-  using G = FrontGeom<M>;
-  using Node = PfspFrontNode<M>;
-  __shared__ FrontSmem<M> sm;
+template <int M, int NJ = 20>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FrontGeom<M, NJ>::WAVES)))
+void pfsp_front_kernel(PfspFrontArgs<M, NJ> a, int t) {
+  using G = FrontGeom<M, NJ>;
+  using Node = PfspFrontNode<M, NJ>;
+  __shared__ FrontSmem<M, NJ> sm;
   const int tid = threadIdx.x;
   const auto& pa = a.pool;
   front_stamp(a, 0);
@@ -1133,17 +1164,17 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
   __syncthreads();
   front_stamp(a, 2);
   if (v.dyn) {
-    front_dyn<M>(a, sm, v, t, best);
+    front_dyn<M, NJ>(a, sm, v, t, best);
     front_stamp(a, 15);
     return;
   }
   if (v.local) {
-    front_local<M>(a, sm, v, t, best);
+    front_local<M, NJ>(a, sm, v, t, best);
     front_stamp(a, 15);
     return;
   }
   if (v.fused) {
-    front_multi_level<M>(a, sm, v, t, best);
+    front_multi_level<M, NJ>(a, sm, v, t, best);
     return;
   }
   for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
@@ -1151,30 +1182,31 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
     uint32_t w[G::NW];
 #pragma unroll
     for (int i = 0; i < G::NW; ++i) w[i] = 0;
-    if (gi < v.B) front_load<M>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
+    if (gi < v.B) front_load<M, NJ>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
     const bool first = ch == static_cast<int>(blockIdx.x);
     const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
     // children this rank keeps (all of them outside the split iteration)
-    uint32_t kmask = ~0u;
+    using Mask = typename G::Mask;
+    Mask kmask = ~Mask(0);
     if (v.split) {
       kmask = 0;
-      for (uint32_t x = w[1]; x; x &= x - 1) {
-        const int j = __builtin_ctz(x);
-        kmask |= split_keep(v, gi, j) ? (1u << j) : 0u;
+      for (Mask x = front_mask<M, NJ>(w); x; x &= x - 1) {
+        const int j = mask_ctz(x);
+        kmask |= split_keep(v, gi, j) ? (Mask(1) << j) : Mask(0);
       }
     }
-    uint32_t surv = 0;
+    Mask surv = 0;
     int nsurv = 0, nleaf = 0;
-    front_parent<M>(
+    front_parent<M, NJ>(
         a, sm, w,
         [&](int j, int lb) {
-          const bool keep = (kmask >> j) & 1u;
+          const bool keep = (kmask >> j) & Mask(1);
           if (leaf) {
             nleaf += keep;
             if (lb < best) atomicMin(&pa.ctl->best.v, lb);
           } else if (keep && lb < best) {
             ++nsurv;
-            surv |= 1u << j;
+            surv |= static_cast<typename G::Mask>(1) << j;
           }
         },
         v.split ? kDbgSplit : kDbgOne);
@@ -1188,7 +1220,7 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
       lcnt_out[ch] = (tot >> 13) & 0x1ff;
     }
     if (first) front_stamp(a, 5);
-    front_emit<M>(sm, w, surv, reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off));
+    front_emit<M, NJ>(sm, w, surv, reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT + off));
     if (first) front_stamp(a, 6);
   }
   front_stamp(a, 15);
@@ -1196,19 +1228,20 @@ void pfsp_front_kernel(PfspFrontArgs<M> a, int t) {
 
 // Reference-style evaluation for the tests (ref evaluate_gpu, PFSP_gpu_lib.cu:129-152):
 // bounds of every child of every parent, in ascending job order per parent.
-template <int M>
-__global__ __launch_bounds__(kBlock) void pfsp_front_bounds_kernel(PfspFrontArgs<M> a) {
-  using G = FrontGeom<M>;
-  __shared__ FrontSmem<M> sm;
+template <int M, int NJ = 20>
+__global__ __launch_bounds__(kBlock) void pfsp_front_bounds_kernel(PfspFrontArgs<M, NJ> a) {
+  using G = FrontGeom<M, NJ>;
+  __shared__ FrontSmem<M, NJ> sm;
   uint16_t* pt = &sm.ptab[0][0];
   for (int i = threadIdx.x; i < a.jobs * G::MS; i += kBlock) pt[i] = a.ptab[i];
   __syncthreads();
   for (int i = blockIdx.x * kBlock + threadIdx.x; i < a.nparents; i += gridDim.x * kBlock) {
     uint32_t w[G::NW];
-    front_load<M>(a.parents_in + i, w);
-    const uint32_t rest = w[1];
+    front_load<M, NJ>(a.parents_in + i, w);
+    using Mask = typename G::Mask;
+    const Mask rest = front_mask<M, NJ>(w);
     int* out = a.bounds_out + a.offsets[i];
-    front_parent<M>(a, sm, w, [&](int j, int lb) { out[__popc(rest & ((1u << j) - 1u))] = lb; });
+    front_parent<M, NJ>(a, sm, w, [&](int j, int lb) { out[mask_pop(rest & ((Mask(1) << j) - Mask(1)))] = lb; });
   }
 }
 

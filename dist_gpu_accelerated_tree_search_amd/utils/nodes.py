@@ -2,7 +2,8 @@
 
 PFSP node (csrc/core/pfsp_node.hpp): id_t depth; id_t prmu[NJ]; padded to 16 B,
 id_t = uint8 for NJ <= 255 else uint16. PFSP front node (LB1 / LB1_d engines on up to
-20 jobs): uint8 depth, 3 pad, uint32 unscheduled-job mask, uint16 front[MB], padded
+20 jobs): uint8 depth, 3 pad, uint32 unscheduled-job mask, uint16 front[MB] (21-50 jobs:
+7 pad and a uint64 mask), padded
 to 16 B (32 B for MB <= 10 machines, 48 B for 20). N-Queens node: 4 x uint32
 {cols, diag, anti, depth}. Parity: ref pfsp/lib/PFSP_node.h:15-20 (44-B node with
 limit1 stored), nqueens/lib/NQueens_node.h:13-17 (board).
@@ -57,12 +58,19 @@ def pfsp_root(jobs: int) -> np.ndarray:
     return pfsp_pack([0], [np.arange(jobs)], jobs)
 
 
-def pfsp_front_unpack(nodes: np.ndarray, machines_bucket: int):
-    """Front nodes -> (depths[n], rest masks[n], fronts[n, machines_bucket])."""
+def pfsp_front_unpack(nodes: np.ndarray, machines_bucket: int, jobs: int = 20):
+    """Front nodes -> (depths[n], rest masks[n], fronts[n, machines_bucket]). Up to 20
+    jobs the unscheduled set is 32 bits at byte 4 and the fronts start at byte 8; up to
+    50 jobs it is 64 bits at byte 8 and the fronts start at byte 16."""
     a = np.ascontiguousarray(nodes, dtype=np.uint8)
     depths = a[:, 0].astype(np.int64)
-    rest = a[:, 4:8].copy().view(np.uint32).reshape(-1).astype(np.int64)
-    fronts = a[:, 8:8 + 2 * machines_bucket].copy().view(np.uint16).astype(np.int64)
+    if jobs <= 20:
+        rest = a[:, 4:8].copy().view(np.uint32).reshape(-1).astype(np.int64)
+        f0 = 8
+    else:
+        rest = a[:, 8:16].copy().view(np.uint64).reshape(-1)
+        f0 = 16
+    fronts = a[:, f0:f0 + 2 * machines_bucket].copy().view(np.uint16).astype(np.int64)
     return depths, rest, fronts
 
 

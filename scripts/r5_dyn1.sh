@@ -1,6 +1,6 @@
 set -o pipefail
 out=gpurun_out/r5dyn1; mkdir -p $out
-timeout -k 10 500 python -u -m pytest tests/test_gpu_dyn.py tests/test_gpu_rccl.py tests/test_gpu_distributed.py::test_gpu_cli_spawn_two_ranks_one_device -m gpu -x -v --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_dyn.py tests/test_gpu_rccl.py tests/test_gpu_distributed.py::test_gpu_cli_spawn_two_ranks_one_device "tests/test_gpu_kernels.py::test_lb2_expand_path_matches_cpu" -m gpu -x -v --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
 tail -15 $out/tests.log
 for us in 0 30 100 300 2000; do
   TTS_DYN_US=$us timeout -k 10 120 python bench.py --steps 50 --warmup 10 --no-extras > $out/bench_$us.json 2> $out/bench_$us.err || { tail -20 $out/bench_$us.err; exit 1; }

@@ -26,7 +26,15 @@ def test_layout_sizes():
     assert PfspModel(7, 0).node_bytes == 32                                        # 20 x 5
     assert PfspModel(21, 0).node_bytes == 48                                       # 20 x 20
     assert PfspModel(14, 2).node_bytes == 32 and not PfspModel(14, 2).front_layout  # LB2: permutation
-    assert PfspModel(56, 1).node_bytes == 64 and not PfspModel(56, 1).front_layout  # 50 jobs
+    assert PfspModel(56, 1).node_bytes == 64 and PfspModel(56, 1).front_layout      # 50 x 20: 64-bit job set
+    assert PfspModel(31, 0).node_bytes == 32 and PfspModel(31, 0).front_layout      # 50 x 5
+    assert PfspModel(41, 1).node_bytes == 48                                        # 50 x 10
+    assert PfspModel(56, 2).node_bytes == 64 and not PfspModel(56, 2).front_layout  # LB2: permutation
+    assert PfspModel(61, 1).node_bytes == 112 and not PfspModel(61, 1).front_layout  # 100 jobs: permutation
+    r50 = PfspModel(51, 0).root()
+    d, rest, fr = nd.pfsp_front_unpack(r50, 20, jobs=50)
+    assert d[0] == 0 and int(rest[0]) == (1 << 50) - 1
+    assert list(fr[0]) == list(C.PfspInstance.taillard(51).min_heads)
     root = PfspModel(21, 0).root()
     d, rest, fr = nd.pfsp_front_unpack(root, 20)
     inst = C.PfspInstance.taillard(21)
@@ -34,7 +42,8 @@ def test_layout_sizes():
 
 
 @pytest.mark.parametrize("spec", [(14, None), (7, None), (21, None), (None, (20, 7, 3)), (None, (20, 13, 4)),
-                                  (None, (16, 2, 5)), (None, (12, 20, 6))])
+                                  (None, (16, 2, 5)), (None, (12, 20, 6)), (31, None), (41, None), (51, None),
+                                  (None, (21, 4, 8)), (None, (35, 9, 9)), (None, (50, 17, 10))])
 def test_front_bounds_equal_permutation_bounds(spec):
     inst, syn = spec
     model = PfspModel(inst, 0) if inst else PfspModel.synthetic(*syn, lb=0)
@@ -99,3 +108,19 @@ def test_front_children_of_the_root_start_from_zero():
     for r, f in zip(rest, fr):
         j = [x for x in range(20) if not (int(r) >> x) & 1][0]
         assert list(f) == list(np.cumsum(p[:, j]))
+
+
+@pytest.mark.parametrize("gap,gold", [(170, 5553), (160, None)])
+def test_front_trees_fifty_jobs(gap, gold, monkeypatch):
+    # 50-job front nodes (64-bit job sets) against the permutation layout on ta051 LB1_d
+    # with an incumbent below the optimum (the -u 1 tree is far too large for a test)
+    C = ops.cpu()
+    native = C.PfspInstance.taillard(51)
+    got = {}
+    for front in ("1", "0"):
+        monkeypatch.setenv("TTS_FRONT", front)
+        r = C.run_pfsp(native, 0, native.best_known - gap, threads=2)
+        got[front] = (r["tree"], r["sol"], r["best"])
+    assert got["1"] == got["0"]
+    if gold is not None:
+        assert got["1"][0] == gold

@@ -145,3 +145,17 @@ def test_ta021_subtree_parity_gpu_vs_host():
     r = probe(model, nodes[32:], d["best"], cap=1 << 25)
     check(r, [])
     assert (r["tree"], r["sol"]) == (sum(s["tree"] for s in d["samples"][32:]), sum(s["sol"] for s in d["samples"][32:]))
+
+
+@pytest.mark.parametrize("gap,dyn_us", [(170, 0), (155, 0), (155, 40)])
+def test_front_probe_fifty_jobs(gap, dyn_us):
+    # 50-job front nodes (64-bit job sets, 64-B nodes for 20 machines) on ta051 LB1_d with
+    # an incumbent below the optimum: every bound the kernel evaluates against the host
+    # oracle, and the tree against the host drain of the same start nodes
+    model = PfspModel(51, 0)
+    assert model.front_layout and model.node_bytes == 64
+    nodes, _, _, best = model.warmup(model.best_known - gap, 25)
+    r = probe(model, nodes, best, cap=1 << 25, max_parents=1 << 19, dyn_us=dyn_us)
+    check(r, [])
+    tree, sol, _ = model.drain(best, nodes)
+    assert (r["tree"], r["sol"]) == (tree, sol)
