@@ -527,7 +527,7 @@ FrontProbeResult pfsp_front_probe_t(const PfspInstance& in, int lb, const void* 
     Node parent;
     std::memcpy(&parent, r + 2, sizeof(Node));
     bool bad = false;
-    if (j >= 32 || !((parent.rest >> j) & 1u)) {
+    if (j >= NJ || !((parent.rest >> j) & 1u)) {
       ++res.bad_job;
       bad = true;
     } else {

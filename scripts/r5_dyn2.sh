@@ -1,7 +1,7 @@
 set -o pipefail
-out=gpurun_out/r5dyn1; mkdir -p $out
-timeout -k 10 500 python -u -m pytest tests/test_gpu_dyn.py tests/test_gpu_rccl.py tests/test_gpu_distributed.py::test_gpu_cli_spawn_two_ranks_one_device "tests/test_gpu_kernels.py::test_lb2_expand_path_matches_cpu" tests/test_gpu_front_probe.py -m gpu -x -v --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
-tail -15 $out/tests.log
+out=gpurun_out/r5dyn2; mkdir -p $out
+timeout -k 10 400 python -u -m pytest "tests/test_gpu_front_probe.py::test_front_probe_machine_buckets" "tests/test_gpu_front_probe.py::test_front_probe_fifty_jobs" tests/test_gpu_front_probe.py::test_front_probe_synthetic_machine_padding -m gpu -x -v --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
+grep -E "PASSED|FAILED|SKIPPED" $out/tests.log
 for us in 0 30 100 300 2000; do
   TTS_DYN_US=$us timeout -k 10 120 python bench.py --steps 50 --warmup 10 --no-extras > $out/bench_$us.json 2> $out/bench_$us.err || { tail -20 $out/bench_$us.err; exit 1; }
   python3 -c "import json;d=json.load(open('$out/bench_$us.json'));print('dyn_us $us', round(d['ms_per_step'],4), 'ms', d['config']['tree'])"
@@ -12,9 +12,7 @@ for us in 0 300; do
   grep -v amdgpu.ids $out/ilog_$us.txt
 done
 cp /tmp/base.so $mod
-set -o pipefail
-out=gpurun_out/r5u0; mkdir -p $out
 for dive in 0 32; do
-  TTS_DIVE=$dive timeout -k 10 200 python -u scripts/live_best_probe.py > $out/u0_dive$dive.txt 2>&1 || { tail -20 $out/u0_dive$dive.txt; exit 1; }
-  grep -v amdgpu.ids $out/u0_dive$dive.txt | tail -20
+  TTS_DIVE=$dive timeout -k 10 200 python -u scripts/live_best_probe.py --worlds 1,2 > $out/u0_dive$dive.txt 2>&1 || { tail -20 $out/u0_dive$dive.txt; exit 1; }
+  grep -v amdgpu.ids $out/u0_dive$dive.txt | tail -12
 done

@@ -88,9 +88,10 @@ def test_front_probe_split_iteration():
     assert (tot_t + t0, tot_s + s0) == (2573652, 2648)
 
 
-@pytest.mark.parametrize("inst,target,take", [(21, 20000, 24), (1, 200000, 1), (11, 5000, 64), (31, 0, 0)])
+@pytest.mark.parametrize("inst,target,take", [(21, 20000, 24), (1, 200000, 1), (11, 5000, 64), (61, 0, 0)])
 def test_front_probe_machine_buckets(inst, target, take):
-    # M = 20 (ta021), 5 (ta001), 10 (ta011) on deep subtrees; ta031 (50 jobs) has no front layout
+    # M = 20 (ta021), 5 (ta001), 10 (ta011) on deep subtrees; ta061 (100 jobs) has no front
+    # layout (50-job instances do: test_front_probe_fifty_jobs)
     model = PfspModel(inst, 0)
     if not model.front_layout:
         with pytest.raises(Exception):
