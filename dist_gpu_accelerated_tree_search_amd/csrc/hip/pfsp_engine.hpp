@@ -663,11 +663,13 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   const double us = 1e3 / std::max(1, rate_khz);
   std::vector<double> out = {ms.front(), ms[ms.size() / 2], static_cast<double>(grid),
                              static_cast<double>(after.slot[1].nch)};
-  // words 12-14 of a workgroup are raw (HW_ID, XCC_ID, local DFS counts: front_stamp)
+  // words 9-10 and 12-14 of a workgroup are raw (dynamic DFS counters and idle ticks,
+  // HW_ID, XCC_ID, local DFS counts: front_stamp / front_dyn)
   for (size_t i = 0; i < blk.size(); ++i) {
     const unsigned long long x = blk[i];
     const size_t k = i % 16;
-    out.push_back(k >= 12 && k <= 14 ? static_cast<double>(x) : (x ? static_cast<double>(x - t0) * us : 0.0));
+    const bool raw = (k >= 12 && k <= 14) || k == 9 || k == 10;
+    out.push_back(raw ? static_cast<double>(x) : (x ? static_cast<double>(x - t0) * us : 0.0));
   }
   return out;
 }

@@ -120,6 +120,7 @@ struct FrontSmem {
   struct {
     unsigned long long deadline;
     long long inner;  // nodes pushed in this iteration and expanded here
+    unsigned long long idle_ticks;  // (probe) time spent waiting for a block
     int flags, dslot, best, claim, claim_n, idle, sweep, pad;
   } dyn;
   // multi-level chunks: two levels of nodes (ping-pong), each node with its remain
@@ -883,6 +884,49 @@ __device__ inline int dyn_take(DynCtl* dc, int qbase, int qx, unsigned want, uns
   return -1;
 }
 
+// Copy n nodes src[0..n) -> dst[0..n) within this workgroup's view (plain loads / stores:
+// both in regions this workgroup alone writes), one node per thread and pass.
+// (rare paths of front_dyn, kept out of line: inlined, their temporaries pushed the
+// step's registers into scratch)
+// mode 0: plain -> plain (this workgroup's own regions); 1: plain -> 8-B agent stores
+// (publish); 2: 8-B agent loads -> plain (claim)
+template <int M, int NJ>
+__device__ __attribute__((noinline)) void dyn_copy(const PfspFrontNode<M, NJ>* src, PfspFrontNode<M, NJ>* dst, int n,
+                                                   int mode) {
+  for (int i = static_cast<int>(threadIdx.x); i < n; i += kBlock) {
+    uint32_t x[FrontGeom<M, NJ>::NW];
+    if (mode == 2)
+      dyn_node_load<M, NJ>(const_cast<PfspFrontNode<M, NJ>*>(src + i), x);
+    else
+      front_load<M, NJ>(src + i, x);
+    if (mode == 1)
+      dyn_node_store<M, NJ>(dst + i, x);
+    else
+      front_store<M, NJ>(reinterpret_cast<uint4*>(dst + i), x);
+  }
+}
+template <int M, int NJ>
+__device__ inline void dyn_copy_own(const PfspFrontNode<M, NJ>* src, PfspFrontNode<M, NJ>* dst, int n) {
+  dyn_copy<M, NJ>(src, dst, n, 0);
+}
+
+// Wave 0 of a workgroup whose stack ran dry: claim a full slot of the partition, polling
+// until one is published, the deadline passes, or no partition workgroup has work and
+// no slot is full (returns slot | n << 16, or -1).
+__device__ __attribute__((noinline)) int dyn_claim_spin(DynCtl* dc, int qbase, int qx, DynCtl::Part* part,
+                                                        unsigned long long deadline) {
+  for (int spin = 0; spin < (1 << 20); ++spin) {
+    const int r = dyn_take(dc, qbase, qx, 2u, 3u);
+    if (r >= 0) return r;
+    int stop = 0;
+    if ((threadIdx.x & (kWave - 1)) == 0)
+      stop = wall_clock64() >= deadline || (dyn_ld(&part->busy) == 0 && dyn_ld(&part->avail) == 0);
+    if (__shfl(stop, 0, kWave)) return -1;
+    __builtin_amdgcn_s_sleep(16);
+  }
+  return -1;
+}
+
 template <int M, int NJ>
 __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>& sm, const IterView& v, int t, int best0) {
   using G = FrontGeom<M, NJ>;
@@ -907,22 +951,24 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
     sm.dyn.inner = 0;
     sm.dyn.claim = -1;
     sm.dyn.idle = 0;
+    sm.dyn.pad = 0;  // (probe: steps | donations << 10 | claims << 20)
+    sm.dyn.idle_ticks = 0;
     dyn_add(&part().busy, 1);
   }
-  int top = 0, nst = 0, best = best0, nleaf = 0;
+  // the stack is stk[base, top): pushes and pops at the top, donations take the bottom
+  // (the oldest, shallowest nodes: the largest subtrees, ref steal-half from the pool's
+  // bottom, pfsp_multigpu_cuda.c:369-372); the top nst nodes are held in LDS
+  int base = 0, top = 0, nst = 0, best = best0, nleaf = 0;
   for (int s = 0;; ++s) {
     uint32_t w[NW], rp[G::HW];
     bool have_r = false;
 #pragma unroll
     for (int i = 0; i < NW; ++i) w[i] = 0;
-    const int claim = s == 0 ? -1 : sm.dyn.claim;
     if (s == 0) {
       const u64 gi = static_cast<u64>(ch) + static_cast<u64>(tid) * static_cast<u64>(v.nchunks);
       if (tid < v.bp && gi < v.B) front_load<M, NJ>(pool_parent<Node, G::SLOT, G::MAXCHUNKS>(pa, v, t, gi, sm.pool), w);
-    } else if (claim >= 0) {
-      if (tid < sm.dyn.claim_n) dyn_node_load<M, NJ>(region(claim) + tid, w);
     } else {
-      const int npop = min(top, kBlock);
+      const int npop = min(top - base, kBlock);
       if (tid < npop) {
         const int k = tid - (npop - nst);
         if (k >= 0) {
@@ -944,6 +990,11 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
       top -= npop;
       if (tid == 0) sm.dyn.inner += npop;
     }
+    // the partition's demand and the incumbent, requested now and read after the step
+    // (their round trips overlap the step instead of following it)
+    u64 q_ha = 0;  // hungry | avail << 32
+    if (tid == 0) q_ha = __hip_atomic_load(reinterpret_cast<u64*>(&part().hungry), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
     typename G::Mask surv = 0;
     int nsurv = 0;
     const bool leaf = static_cast<int>(w[0] & 0xffu) + 1 == a.jobs;
@@ -962,9 +1013,8 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
         kDbgDyn);
     int tot = 0;
     const int off = block_exclusive_scan(nsurv, sm.scan, &tot);
-    // (the scan's barrier: every thread holds its node in registers; a claimed slot is read)
     const int tnew = top + tot;
-    nst = min(tot, min(tnew, kBlock));  // the next pop stays in LDS
+    nst = min(tot, min(tnew - base, kBlock));  // the next pop stays in LDS
     const int lo = tot - nst;
     uint4* const dst = reinterpret_cast<uint4*>(stk + top);
     front_emit_to<M, NJ>(sm, w, surv, [&](int i, const uint32_t (&c)[NW], int j) {
@@ -979,24 +1029,18 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
       }
     });
     top = tnew;
-    // wave 0 decides what follows: free a claimed slot, stop at the deadline, publish the
-    // next pop when partition workgroups wait for more blocks than are full (or when the
-    // stack nears the end of its region)
+    // wave 0 decides what follows: stop at the deadline; publish the bottom half of the
+    // stack (up to a slot region's worth below the LDS-held top) when partition
+    // workgroups wait for more blocks than are full, or when the stack nears its end
     if (tid < kWave) {
       int flags = 0, dslot = -1;
-      if (tid == 0) {
-        if (claim >= 0) {
-          sm.dyn.inner += sm.dyn.claim_n;
-          dyn_stu(&pa.dyn[t % 3].st[qslot(claim)], 0u);
-        }
-        if (wall_clock64() >= sm.dyn.deadline) flags = 1;
-      }
+      if (tid == 0 && wall_clock64() >= sm.dyn.deadline) flags = 1;
       flags = __shfl(flags, 0, kWave);
-      if (!flags && top >= 2 * kBlock) {
-        int want = 0;
-        if (tid == 0)
-          want = top + kBlock * (G::NJ - 1) > G::SLOT || dyn_ld(&part().hungry) > dyn_ld(&part().avail);
-        if (__shfl(want, 0, kWave)) {
+      if (!flags && top - base >= 2 * kBlock) {
+        const int q_h = static_cast<int>(static_cast<uint32_t>(q_ha)), q_a = static_cast<int>(q_ha >> 32);
+        const int want = __shfl(tid == 0 ? static_cast<int>(q_h > q_a || top + kBlock * (G::NJ - 1) > G::SLOT) : 0, 0,
+                                kWave);
+        if (want) {
           const int r = dyn_take(pa.dyn + t % 3, qslot(0), v.qn / 8, 0u, 1u);
           dslot = r < 0 ? -1 : (r & 0xffff);
         }
@@ -1004,75 +1048,79 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
       if (tid == 0) {
         sm.dyn.flags = flags;
         sm.dyn.dslot = dslot;
-        sm.dyn.claim = -1;
-        sm.dyn.best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the incumbent, every 8th step (other workgroups' leaves lower it: -u 0)
+        sm.dyn.best = (s & 7) == 7 ? __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : best;
       }
     }
     __syncthreads();  // pushes visible to the next pops; decisions in sm.dyn
     if (s < 4) front_stamp(a, 4 + s);
     best = min(best, sm.dyn.best);
-    if (sm.dyn.dslot >= 0) {
-      const int n = min(top, kBlock);
-      if (tid < n) {
-        uint32_t x[NW];
-        const int k = tid - (n - nst);
-        if (k >= 0) {
-#pragma unroll
-          for (int q = 0; q < G::VPN; ++q) {
-            const uint4 y = sm.stage[k][q];
-            x[4 * q] = y.x;
-            x[4 * q + 1] = y.y;
-            x[4 * q + 2] = y.z;
-            x[4 * q + 3] = y.w;
-          }
-        } else {
-          front_load<M, NJ>(stk + (top - n + tid), x);
-        }
-        dyn_node_store<M, NJ>(region(sm.dyn.dslot) + tid, x);
-      }
+    const int dslot = sm.dyn.dslot;
+    if (dslot >= 0) {
+      // the bottom half (the LDS-held top is above it: top - base >= 2 kBlock >= 2 nst)
+      const int n = min((top - base) / 2, G::SLOT);
+      dyn_copy<M, NJ>(stk + base, region(dslot), n, 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload is complete
       __syncthreads();
       if (tid == 0) {
-        dyn_stu(&pa.dyn[t % 3].st[qslot(sm.dyn.dslot)], 2u | (static_cast<unsigned>(n) << 8));
+        dyn_stu(&pa.dyn[t % 3].st[qslot(dslot)], 2u | (static_cast<unsigned>(n) << 8));
         dyn_add(&part().avail, 1);
+        sm.dyn.pad += 1 << 10;
       }
-      top -= n;
-      nst = 0;
+      base += n;
     }
+    if (tid == 0) sm.dyn.pad += 1;
     if (sm.dyn.flags) break;
-    if (top + kBlock * (G::NJ - 1) > G::SLOT) break;  // a full pop could overflow the region
-    if (top == 0) {
+    if (top + kBlock * (G::NJ - 1) > G::SLOT) {
+      // a full pop could overflow the region: move the stack down to its start
+      if (base == 0) break;
+      const int n = top - nst - base;  // (the LDS-held top moves with top)
+      for (int c = 0; c < n; c += base) {
+        dyn_copy_own<M, NJ>(stk + base + c, stk + c, min(base, n - c));
+        __syncthreads();
+      }
+      top -= base;
+      base = 0;
+      if (top + kBlock * (G::NJ - 1) > G::SLOT) break;
+    }
+    if (top == base) {
       // stack dry: claim a published block of the partition (wave 0; the others wait)
       if (tid < kWave) {
+        const u64 t_idle = wall_clock64();
         if (tid == 0 && !sm.dyn.idle) {
           dyn_add(&part().busy, -1);
           dyn_add(&part().hungry, 1);
           sm.dyn.idle = 1;
         }
-        int r = -1;
-        for (int spin = 0; spin < (1 << 20); ++spin) {
-          r = dyn_take(pa.dyn + t % 3, qslot(0), v.qn / 8, 2u, 3u);
-          if (r >= 0) break;
-          int stop = 0;
-          if (tid == 0)
-            stop = wall_clock64() >= sm.dyn.deadline || (dyn_ld(&part().busy) == 0 && dyn_ld(&part().avail) == 0);
-          if (__shfl(stop, 0, kWave)) break;
-          __builtin_amdgcn_s_sleep(16);
-        }
+        const int r = dyn_claim_spin(pa.dyn + t % 3, qslot(0), v.qn / 8, &part(), sm.dyn.deadline);
         if (tid == 0 && r >= 0) {
           dyn_add(&part().busy, 1);
           dyn_add(&part().hungry, -1);
           dyn_add(&part().avail, -1);
           sm.dyn.idle = 0;
-          sm.dyn.claim = r & 0xffff;
-          sm.dyn.claim_n = r >> 16;
+          sm.dyn.pad += 1 << 20;
+        }
+        if (tid == 0) {
+          sm.dyn.claim = r;
+          sm.dyn.idle_ticks += wall_clock64() - t_idle;
         }
       }
       __syncthreads();
-      if (sm.dyn.claim < 0) break;
+      const int r = sm.dyn.claim;
+      if (r < 0) break;
+      // the block becomes this workgroup's stack
+      const int q = r & 0xffff, n = r >> 16;
+      dyn_copy<M, NJ>(region(q), stk, n, 2);
+      __syncthreads();  // the block is read (and the copy visible to the next pops)
+      if (tid == 0) dyn_stu(&pa.dyn[t % 3].st[qslot(q)], 0u);
+      base = 0;
+      top = n;
+      nst = 0;
     }
   }
-  // the nodes staged for a next step are the top of the stack
+  // the nodes staged for a next step are the top of the stack; then the stack moves to
+  // the start of the region (the chunk's output)
   if (tid < nst) {
     uint32_t x[NW];
 #pragma unroll
@@ -1085,21 +1133,32 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
     }
     front_store<M, NJ>(reinterpret_cast<uint4*>(stk + (top - nst + tid)), x);
   }
+  __syncthreads();
+  if (base > 0) {
+    const int n = top - base;
+    for (int c = 0; c < n; c += base) {
+      dyn_copy_own<M, NJ>(stk + base + c, stk + c, min(base, n - c));
+      __syncthreads();
+    }
+  }
   int leaves = 0;
   (void)block_exclusive_scan(nleaf, sm.scan, &leaves);
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
   if (tid == 0) {
     dyn_add(sm.dyn.idle ? &part().hungry : &part().busy, -1);
-    cnt_out[ch] = top;
+    cnt_out[ch] = top - base;
     lcnt_out[ch] = 0;
     auto& x = pa.ctl->xacc[ch & 7];
     const long long inner = sm.dyn.inner;
     if (inner) __hip_atomic_fetch_add(&x.tree, static_cast<u64>(inner), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (leaves) __hip_atomic_fetch_add(&x.sol, static_cast<u64>(leaves), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.dbg_blk)
+    if (a.dbg_blk) {
       a.dbg_blk[blockIdx.x * 16 + 14] = static_cast<unsigned long long>(inner) |
-                                        (static_cast<unsigned long long>(top) << 32);
+                                        (static_cast<unsigned long long>(top - base) << 32);
+      a.dbg_blk[blockIdx.x * 16 + 9] = static_cast<unsigned long long>(static_cast<unsigned>(sm.dyn.pad));
+      a.dbg_blk[blockIdx.x * 16 + 10] = sm.dyn.idle_ticks;
+    }
     // the last workgroup out (every slot state final) writes the queue chunks' counts
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     DynCtl* const dc = pa.dyn + t % 3;

@@ -80,9 +80,9 @@ struct PoolCtl {
 constexpr int kDynQMax = 1024;
 struct DynCtl {
   struct alignas(128) Part {
+    int hungry;  // workgroups of the partition waiting for a block
+    int avail;   // full slots (hungry and avail: one 8-B load)
     int busy;    // workgroups of the partition with work (a stack or a claimed block)
-    int hungry;  // ... waiting for a block
-    int avail;   // full slots
     int pad[29];
   } part[8];
   struct alignas(128) Fin {

@@ -1,7 +1,7 @@
 """Where does a local-DFS front kernel's tail come from? Per-workgroup stamps plus the
 hardware placement (HW_ID / XCC_ID read at entry) of one timed iteration per window.
 
-    python scripts/lb_probe.py [inst] [depths] [steps]
+    python scripts/lb_probe.py [inst] [depths] [steps] [dyn_us]
 
 For each ta014 BFS window (depth d): the exit-time spread over workgroups, the same
 grouped by CU (max exit per CU: is the kernel bound by one slow workgroup or by whole
@@ -22,6 +22,7 @@ from dist_gpu_accelerated_tree_search_amd.models.pfsp import PfspModel  # noqa: 
 inst = int(sys.argv[1]) if len(sys.argv) > 1 else 14
 depths = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [9, 11, 13, 15]
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+dyn_us = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 m = PfspModel(inst, 1)
 H = ops.require_gpu(0)
 best = m.best_known
@@ -38,7 +39,7 @@ for dep in depths:
     if len(nodes) == 0:
         continue
     d = H.pfsp_front_time(m.jobs, m.machines, list(m.native.p), m.lb, nodes, best, reps=10, local_min=1,
-                          local_steps=steps)
+                          local_steps=steps, dyn_us=dyn_us)
     st = d["stamps_us"]
     ent, ex = st[:, 0], st[:, 15]
     live = ex > 0
@@ -87,5 +88,13 @@ for dep in depths:
         steps_t.append(f"step{k - 4} n={ok.sum()} {dt.mean():.1f}/{np.percentile(dt, 90):.1f}/{dt.max():.1f}")
         prev = np.where(ok, col, prev)
     print("  " + " | ".join(steps_t), flush=True)
+    if dyn_us:
+        cw = st[live, 9].astype(np.int64)
+        nstep, ndon, ncl = cw & 0x3FF, (cw >> 10) & 0x3FF, (cw >> 20) & 0x3FF
+        idle = st[live, 10] / 100.0  # 100 MHz ticks -> us
+        print(f"  dyn: steps p10/50/90/max {np.percentile(nstep, [10, 50, 90, 100]).astype(int).tolist()} "
+              f"donations total {int(ndon.sum())} (wgs {int((ndon > 0).sum())}) claims total {int(ncl.sum())} "
+              f"idle us mean {idle.mean():.1f} max {idle.max():.1f}; left on stacks {int(left[live].sum())}",
+              flush=True)
     if os.environ.get("TTS_PROBE_DUMP"):
         np.save(f"gpurun_out/lb_probe_d{dep}.npy", st)
