@@ -910,6 +910,13 @@ __device__ inline void dyn_copy_own(const PfspFrontNode<M, NJ>* src, PfspFrontNo
   dyn_copy<M, NJ>(src, dst, n, 0);
 }
 
+// A stack of at least this many nodes gives its bottom half to a waiting workgroup of its
+// partition. Splitting small frontiers (64) balanced the per-CU work (p90/p10 1.35) but
+// slowed every budget (ta014 headline 0.354 / 0.504 ms at 40 / 300 us against 0.238 / 0.332
+// with 512): the thieves' steps are short and each step costs its full latency
+// (profiles/r5/dyn_eager_ab.txt)
+constexpr int kDynMinDonate = 512;
+
 // Wave 0 of a workgroup whose stack ran dry: claim a full slot of the partition, polling
 // until one is published, the deadline passes, or no partition workgroup has work and
 // no slot is full (returns slot | n << 16, or -1).
@@ -1036,7 +1043,7 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
       int flags = 0, dslot = -1;
       if (tid == 0 && wall_clock64() >= sm.dyn.deadline) flags = 1;
       flags = __shfl(flags, 0, kWave);
-      if (!flags && top - base >= 2 * kBlock) {
+      if (!flags && top - base >= kDynMinDonate) {
         const int q_h = static_cast<int>(static_cast<uint32_t>(q_ha)), q_a = static_cast<int>(q_ha >> 32);
         const int want = __shfl(tid == 0 ? static_cast<int>(q_h > q_a || top + kBlock * (G::NJ - 1) > G::SLOT) : 0, 0,
                                 kWave);
@@ -1058,8 +1065,25 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
     best = min(best, sm.dyn.best);
     const int dslot = sm.dyn.dslot;
     if (dslot >= 0) {
-      // the bottom half (the LDS-held top is above it: top - base >= 2 kBlock >= 2 nst)
+      // the bottom half; when the LDS-held top reaches into it, the stage goes to the
+      // stack first (its place in the region is free: pops and pushes at the top)
       const int n = min((top - base) / 2, G::SLOT);
+      if (base + n > top - nst) {
+        if (tid < nst) {
+          uint32_t x[NW];
+#pragma unroll
+          for (int q = 0; q < G::VPN; ++q) {
+            const uint4 y = sm.stage[tid][q];
+            x[4 * q] = y.x;
+            x[4 * q + 1] = y.y;
+            x[4 * q + 2] = y.z;
+            x[4 * q + 3] = y.w;
+          }
+          front_store<M, NJ>(reinterpret_cast<uint4*>(stk + (top - nst + tid)), x);
+        }
+        nst = 0;
+        __syncthreads();
+      }
       dyn_copy<M, NJ>(stk + base, region(dslot), n, 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload is complete
       __syncthreads();
