@@ -718,6 +718,16 @@ __device__ inline void front_local(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, N
     // step's last children, exactly the ones this step pops) instead of the slot region
     int top = 0, pushed = 0, nleaf = 0, nst = 0;
     for (int s = 0; s < v.steps; ++s) {
+      // Wave priority falls with the step: workgroups behind in steps issue first. A CU
+      // otherwise issues its oldest waves first, so late-dispatched workgroups trailed
+      // (exit vs dispatch rank in the CU r = 0.93) and each CU's tail ran with few waves
+      // on a latency-bound loop. ta014 window exits max/mean 1.50 -> 1.20, headline
+      // 0.2182 -> 0.2021 ms, ta021 one engine 16.3 -> 14.1 s; a stack-size priority
+      // gained nothing (profiles/r5/prio_ab.txt)
+      if (s == 0) __builtin_amdgcn_s_setprio(3);
+      else if (s == 1) __builtin_amdgcn_s_setprio(2);
+      else if (s == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
       uint32_t w[G::NW], rp[G::HW];
       bool have_r = false;  // rp carried with a staged node
 #pragma unroll

@@ -14,7 +14,7 @@ for r in $(seq 1 "$reps"); do
 lines=[l for l in sys.stdin.read().splitlines() if l.strip()]
 try:
     d=json.loads(lines[-1])
-    ex=' '.join('%s %.3f s' % (k, e['seconds']) for k, e in d.get('extras', {}).items() if 'seconds' in e)
+    ex=' '.join(('%s %.3f s %.4f Gn/s' % (k, e['seconds'], e.get('nodes_per_s', 0) / 1e9)) for k, e in d.get('extras', {}).items() if 'seconds' in e)
     print('$v run $r: %.4f ms/step %s' % (d['ms_per_step'], ex))
 except Exception:
     print('\n'.join('$v run $r: '+l for l in lines))"
