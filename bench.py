@@ -304,7 +304,13 @@ def run_solve_extra(a, comm, device: int, inst: int, lb: int, time_limit: float)
     d = {"config": name, "n_gpus": comm.world, "seconds": dt, "tree": r.tree, "sol": r.sol, "makespan": r.best,
          "nodes_per_s": r.tree / dt, "complete": bool(r.extra.get("complete", True)),
          "rounds": r.extra.get("rounds"), "per_rank_tree": [w.tree for w in r.workers],
-         "engine_setup_s": t_setup, "engines_per_gpu": max(1, a.extra_streams), "max_parents": opts.max_parents}
+         "engine_setup_s": t_setup, "engines_per_gpu": max(1, a.extra_streams), "max_parents": opts.max_parents,
+         # where the ranks' time went (the round loop's clocks): idle without work, load
+         # balancing (plan + transfers), termination checks; rounds that overlapped replays
+         "per_rank_t_idle": [round(w.t_idle, 4) for w in r.workers],
+         "per_rank_t_load_bal": [round(w.t_load_bal, 4) for w in r.workers],
+         "per_rank_t_termination": [round(w.t_termination, 4) for w in r.workers],
+         "overlapped_rounds": r.extra.get("overlapped_rounds")}
     if time_limit > 0:
         d["time_box_s"] = time_limit
     else:

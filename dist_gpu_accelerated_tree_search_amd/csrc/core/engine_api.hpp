@@ -27,7 +27,10 @@ struct EngineConfig {
   int iters_large = 48;                  // iterations per large graph (multiple of 6)
   int iters_first = 18;                  // first replay after begin(): covers a 20-job tree in one graph
   int fuse_max = 1 << 30;                // two-level iterations for windows up to this many parents (0: off)
-  int local_steps = 4;                   // local DFS steps per chunk and iteration (<= 1: off; capped per kernel)
+  // local DFS steps per chunk and iteration (<= 1: off; capped per kernel). 6 under the
+  // step priority (ta014 0.205 -> 0.198 ms, 5 / 7 / 8 slower; ta021 3 engines 10.1 -> 9.6 s;
+  // profiles/r5/steps_ab.txt)
+  int local_steps = 6;
   // local DFS iterations once the pool holds this many parents (-1: the kernel's default,
   // Traits::kLocalMin; 0: four grid-filling windows)
   int local_min = -1;

@@ -160,8 +160,6 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);
     pa.local_wide_steps = 3;
     if (const char* f = std::getenv("TTS_LOCAL_WIDE_STEPS")) pa.local_wide_steps = std::atoi(f);
-    pa.local_narrow_steps = 6;
-    if (const char* f = std::getenv("TTS_LOCAL_NARROW_STEPS")) pa.local_narrow_steps = std::atoi(f);
     // dynamic local DFS iterations (kernels that have them, Traits::kDyn): 3 control
     // sets, a time budget per iteration (cfg dyn_us, TTS_DYN_US; 0 = fixed-step local
     // iterations) and the queue slots left after one chunk per resident workgroup

@@ -599,7 +599,6 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   pa.local_cap = 0;
   pa.local_stride = 0;
   pa.local_wide_steps = 0;
-  pa.local_narrow_steps = 0;
   if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);
   pa.deep_levels = cfg.deep_levels;
   pa.deep_per[0] = cfg.deep_per3;

@@ -724,9 +724,11 @@ __device__ inline void front_local(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, N
       // on a latency-bound loop. ta014 window exits max/mean 1.50 -> 1.20, headline
       // 0.2182 -> 0.2021 ms, ta021 one engine 16.3 -> 14.1 s; a stack-size priority
       // gained nothing (profiles/r5/prio_ab.txt)
-      if (s == 0) __builtin_amdgcn_s_setprio(3);
-      else if (s == 1) __builtin_amdgcn_s_setprio(2);
-      else if (s == 2) __builtin_amdgcn_s_setprio(1);
+      // (4 levels spread over the steps)
+      const int lvl = min(3, ((v.steps - 1 - s) * 4) / v.steps);
+      if (lvl == 3) __builtin_amdgcn_s_setprio(3);
+      else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+      else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
       uint32_t w[G::NW], rp[G::HW];
       bool have_r = false;  // rp carried with a staged node

@@ -527,19 +527,9 @@ struct PfspSmemLB2 {
   int off[G::BP];
   typename G::map_t map[G::MAXCH];
   uint16_t ptab[NJ][C::MS];
-  // Active slots s are stored parity-split: even slots first, odd ones from HALF on
-  // (li / mi). The packed walks' lane k reads slots 2k and 2k + 1, which in slot order
-  // were 8 B (lbv) and 16 B (cm) apart: 2-way bank conflicts on every read and atomic
-  // (ta056: 1.11 conflict cycles per LDS instruction, profiles/r4/pmc/ta056_summary.txt).
-  // lbv's odd half starts 32 banks on, so lanes reading consecutive slots (the per-child
-  // walks) also fall on distinct banks.
-  static constexpr int HALF = (G::MAXCH + 1) / 2;
-  static constexpr int LHALF = HALF <= 32 ? 32 : ((HALF - 32 + 63) / 64) * 64 + 32;
-  __device__ static constexpr int li(int s) { return (s & 1) * LHALF + (s >> 1); }
-  __device__ static constexpr int mi(int s) { return (s & 1) * HALF + (s >> 1); }
   uint16_t cf[M][G::MAXCH];               // active child fronts, machine-major
-  u64 cm[2 * HALF][G::NW];                // active child scheduled sets (mi)
-  int lbv[LHALF + HALF];                  // active child LB2, max over pairs (li)
+  u64 cm[G::MAXCH][G::NW];                // active child scheduled sets
+  int lbv[G::MAXCH];                      // active child LB2 (max over pairs)
   int16_t act[G::MAXCH];                  // child -> active slot, -1 if decided in B1
   int16_t alist[G::MAXCH];                // B2 rounds: active slots still below best
   uint8_t aparent[G::MAXCH];              // active slot -> chunk parent
@@ -841,8 +831,8 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         for (int m = 0; m < M; ++m) sm.cf[m][slot] = static_cast<uint16_t>(f[m]);
 #pragma unroll
         for (int w = 0; w < G::NW; ++w)
-          sm.cm[S::mi(slot)][w] = sm.pmask[p][w] | (((job >> 6) == w) ? (1ull << (job & 63)) : 0ull);
-        sm.lbv[S::li(slot)] = 0;
+          sm.cm[slot][w] = sm.pmask[p][w] | (((job >> 6) == w) ? (1ull << (job & 63)) : 0ull);
+        sm.lbv[slot] = 0;
         sm.aparent[slot] = static_cast<uint8_t>(p);
         sm.ajob[slot] = static_cast<uint8_t>(job);
       }
@@ -875,7 +865,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
           while (qq < nq) {
             const int ca = sm.alist[2 * kk];
             const int cb = 2 * kk + 1 < na ? sm.alist[2 * kk + 1] : -1;
-            const bool la = sm.lbv[S::li(ca)] < best, lbb = cb >= 0 && sm.lbv[S::li(cb)] < best;
+            const bool la = sm.lbv[ca] < best, lbb = cb >= 0 && sm.lbv[cb] < best;
             if (la || lbb) {
               const uint2 pi = sm.pinfo[q0 + qq];
               const int m0 = pi.x & 0xff, m1 = (pi.x >> 8) & 0xff;
@@ -884,21 +874,21 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
               uint32_t t1 = static_cast<uint32_t>(sm.cf[m1][ca]) | (static_cast<uint32_t>(sm.cf[m1][cbb]) << 16);
               if constexpr (G::NW > 2) {
                 // (a lone child walks in both halves; the second half's result is unused)
-                lb2_walk_pipe2_lds(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, sm.cm[S::mi(ca)],
-                                   sm.cm[S::mi(cbb)], t0, t1);
+                lb2_walk_pipe2_lds(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, sm.cm[ca],
+                                   sm.cm[cbb], t0, t1);
               } else {
                 u64 ma[G::NW], mb[G::NW];
 #pragma unroll
                 for (int w = 0; w < G::NW; ++w) {
-                  ma[w] = sm.cm[S::mi(ca)][w];
-                  mb[w] = cb >= 0 ? sm.cm[S::mi(cbb)][w] : ~0ull;
+                  ma[w] = sm.cm[ca][w];
+                  mb[w] = cb >= 0 ? sm.cm[cbb][w] : ~0ull;
                 }
                 lb2_walk_pipe2(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, ma, mb, t0, t1);
               }
               const int tl0 = static_cast<int>(pi.y & 0xffff), tl1 = static_cast<int>(pi.y >> 16);
               if (la)
-                atomicMax(&sm.lbv[S::li(ca)], max(static_cast<int>(t1 & 0xffff) + tl1, static_cast<int>(t0 & 0xffff) + tl0));
-              if (lbb) atomicMax(&sm.lbv[S::li(cb)], max(static_cast<int>(t1 >> 16) + tl1, static_cast<int>(t0 >> 16) + tl0));
+                atomicMax(&sm.lbv[ca], max(static_cast<int>(t1 & 0xffff) + tl1, static_cast<int>(t0 & 0xffff) + tl0));
+              if (lbb) atomicMax(&sm.lbv[cb], max(static_cast<int>(t1 >> 16) + tl1, static_cast<int>(t0 >> 16) + tl0));
             }
             kk += dk;
             qq += dq;
@@ -917,17 +907,17 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
           const int uref = __ballot(qq != qf) == 0
                                ? __builtin_amdgcn_readfirstlane(static_cast<int>(sm.pinfo[q0 + qf].x >> 16))
                                : -1;
-          if (sm.lbv[S::li(ai)] < best) {
+          if (sm.lbv[ai] < best) {
             const uint2 pi = sm.pinfo[q0 + qq];
             int t0 = sm.cf[pi.x & 0xff][ai], t1 = sm.cf[(pi.x >> 8) & 0xff][ai];
             u64 msk[G::NW];
 #pragma unroll
-            for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[S::mi(ai)][w];
+            for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
             if (pipe && uref < 0)
               lb2_walk_pipe<G::NW>(a.recs4 + static_cast<int>(pi.x >> 16) * a.rs4, ndouble, msk, t0, t1);
             else
               lb2_johnson_walk<NJ, M, S>(recs, pi, N, msk, t0, t1, uref);
-            atomicMax(&sm.lbv[S::li(ai)], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
+            atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
           }
           ii += di;
           qq += dq;
@@ -947,7 +937,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         for (int k = 0; k < PER; ++k) {
           const int i = k * kBlock + tid;
           ent[k] = i < na ? sm.alist[i] : -1;
-          kp[k] = ent[k] >= 0 && sm.lbv[S::li(ent[k])] < best;
+          kp[k] = ent[k] >= 0 && sm.lbv[ent[k]] < best;
         }
         int nn = 0;
 #pragma unroll
@@ -967,14 +957,14 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
         const int qf = __builtin_amdgcn_readfirstlane(q);
         const int uref =
             __ballot(q != qf) == 0 ? __builtin_amdgcn_readfirstlane(static_cast<int>(sm.pinfo[qf].x >> 16)) : -1;
-        if (sm.lbv[S::li(ai)] < best) {
+        if (sm.lbv[ai] < best) {
           const uint2 pi = sm.pinfo[q];
           int t0 = sm.cf[pi.x & 0xff][ai], t1 = sm.cf[(pi.x >> 8) & 0xff][ai];
           u64 msk[G::NW];
 #pragma unroll
-          for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[S::mi(ai)][w];
+          for (int w = 0; w < G::NW; ++w) msk[w] = sm.cm[ai][w];
           lb2_johnson_walk<NJ, M, S>(recs, pi, N, msk, t0, t1, uref);
-          atomicMax(&sm.lbv[S::li(ai)], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
+          atomicMax(&sm.lbv[ai], max(t1 + static_cast<int>(pi.y >> 16), t0 + static_cast<int>(pi.y & 0xffff)));
         }
         ai += da;
         q += dq;
@@ -996,10 +986,10 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
       bool survive = false;
       if (c < total) {
         const int s = sm.act[c];
-        survive = s >= 0 && sm.lbv[S::li(s)] < best;
+        survive = s >= 0 && sm.lbv[s] < best;
         if (a.dbg_lb && s >= 0) {
           const int p = sm.map[c];
-          a.dbg_lb[a.dbg_off[gidx(p)] + (c - sm.off[p])] = sm.lbv[S::li(s)];
+          a.dbg_lb[a.dbg_off[gidx(p)] + (c - sm.off[p])] = sm.lbv[s];
         }
       }
       const u64 bal = __ballot(survive);

@@ -110,7 +110,6 @@ struct PoolArgs {
   int local_cap;    // > 0: a local DFS chunk takes no further step once its stack holds more than this
   int local_stride;    // local DFS chunks take strided window parents (ch, ch + nchunks, ...)
   int local_wide_steps;  // > 0: steps of a strided local window of at least 160 parents per workgroup
-  int local_narrow_steps;  // > 0: ... of fewer than 64 parents per workgroup in a split rank share
   // multi-level iterations (kernels with LMAX > 2): a fused window of at most deep_per[0]
   // parents per workgroup is expanded 3 levels deep, of at most deep_per[1] 4 levels deep
   // (capped by deep_levels); 2 levels otherwise
@@ -349,13 +348,9 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   v.stride = v.local && pa.local_stride && v.S + v.C < 4 * full;
   // wide strided windows (a tree's widest levels, full 256-node pops) take fewer steps: a
   // step more there mostly lengthens the slowest workgroup (ta014 one rank: 3 steps 0.215
-  // vs 4 steps 0.219 ms; the narrower windows of 4- and 8-way rank shares keep 4)
+  // vs 4 steps 0.219 ms; under the step priority 3 / 4 / 5 steps 0.206 / 0.210 / 0.215 ms,
+  // profiles/r5/steps_ab.txt)
   if (v.stride && pa.local_wide_steps > 0 && min(v.B, full) >= 160ull * gridDim.x) v.steps = pa.local_wide_steps;
-  // a rank's share after a W-way split (W >= 2): its windows stay a 1/W sample of every
-  // level, so narrow strided windows take more steps (4 / 8-way shares -10 / -8 %); on one
-  // rank a narrow window is the ramp of a tree that widens fast, where they cost (+2 %)
-  if (v.stride && pa.local_narrow_steps > 0 && v.sworld > 1 && done_in && min(v.B, full) < 64ull * gridDim.x)
-    v.steps = pa.local_narrow_steps;
   v.cap = pa.local_cap > 0 ? pa.local_cap : 0x7fffffff;
   // dynamic local DFS: every workgroup owns its chunk (the window dealt strided over the
   // grid) and steps until the time budget, sharing work through the queue slots
