@@ -495,9 +495,16 @@ class DeviceEngine final : public IEngine, public DeviceResource {
       const size_t all = total + spill_.size() + refill_n_;
       if (all == 0) {
         // the tree is done: the next solve's first replay gets this solve's iteration
-        // count (rounded up to whole phases), so it ends without empty iterations
+        // count, so it ends without empty iterations (ta014: 2 empty launches of ~5 us
+        // each when rounded up to whole phases). Dynamic iterations keep whole phases:
+        // their control sets rotate with the slot (dyn_zero_next)
         const dev::u64 it = h_ctl_->iters;
-        learned_k_ = (it >= 3 && it <= 48) ? static_cast<int>((it + 2) / 3 * 3) : 0;
+#ifdef TTS_LEARN_ROUND  // A/B builds: whole phases
+        const bool exact = false;
+#else
+        const bool exact = args_.pool.dyn == nullptr;
+#endif
+        learned_k_ = (it >= 1 && it <= 48) ? static_cast<int>(exact ? it : (it + 2) / 3 * 3) : 0;
         break;
       }
       if (all < stop_below) break;
@@ -690,7 +697,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
       next_mirror_ ^= 1;
       for (int i = 0; i < 6; ++i) Traits::launch(a, i, grid_, stream_);
       a.pool.mirror = d_mirror_[m];
-      Traits::finalize(a.pool, 0, stream_);
+      Traits::finalize(a.pool, 0, 0, stream_);
       TTS_HIP_CHECK(hipGetLastError());
       TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
       push_inflight(m, 6);
@@ -1131,7 +1138,8 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     upload_ctl();
   }
 
-  // Graphs hold 3k iterations, so a replay starts and ends at phase 0 or 3 (iteration t
+  // Graphs hold 3k iterations (learned first replays any count, their finalize moving the
+  // last slot to slot 0), so a replay starts and ends at phase 0 or 3 (iteration t
   // reads slot t % 3 — slot 0 at both — and buffer t & 1): phase_ is the next
   // iteration's t, and every graph exists for both start phases. K < 0: the learned
   // first-replay graph of -K iterations (learn_first_).
@@ -1151,13 +1159,15 @@ class DeviceEngine final : public IEngine, public DeviceResource {
       for (int i = 0; i < k; ++i) Traits::launch(args_, (phase_ + i) % 6, grid_, stream_);
       auto pa = args_.pool;
       pa.mirror = d_mirror_[m];
-      Traits::finalize(pa, ((phase_ + k) % 6) & 1, stream_);
+      Traits::finalize(pa, ((phase_ + k) % 6) & 1, (phase_ + k) % 3, stream_);
       TTS_HIP_CHECK(hipGetLastError());
     }
     TTS_HIP_CHECK(hipEventRecord(graph_done_[m], stream_));
     if (tr) trace_rec_.push_back({0, tr, trace_mark(stream_)});
     push_inflight(m, k);
     phase_ = (phase_ + k) % 6;
+    // (a learned replay of k != 3j iterations: its finalize moved slot k % 3 to slot 0)
+    if (phase_ % 3) phase_ = (phase_ & 1) ? 3 : 0;
     ++stats_.launches;
     fresh_ = false;
   }
@@ -1208,7 +1218,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     for (int i = 0; i < K; ++i) Traits::launch(args_, (phase + i) % 6, grid_, cs);
     auto pa = args_.pool;
     pa.mirror = d_mirror_[mirror];
-    Traits::finalize(pa, ((phase + K) % 6) & 1, cs);
+    Traits::finalize(pa, ((phase + K) % 6) & 1, (phase + K) % 3, cs);
     TTS_HIP_CHECK(hipStreamEndCapture(cs, &g));
     hipGraphExec_t exec;
     TTS_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
@@ -1294,7 +1304,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   std::map<int, std::array<hipGraphExec_t, 2>> first_graphs_;  // learned first replays by length
   int phase_ = 0;         // t of the next iteration: 0 or 3
   bool learn_first_ = true;  // first replay after begin() = the previous solve's iterations (TTS_LEARN_FIRST=0: off)
-  int learned_k_ = 0;     // ... rounded up to 3k (0: unknown)
+  int learned_k_ = 0;     // ... (0: unknown)
   std::vector<void*> owned_;
   hipEvent_t ev_ahead_ = nullptr;  // after the latest export_ahead copy (transfer stream)
   bool ahead_copy_ = false;

@@ -42,8 +42,8 @@ struct PfspTraits {
     hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::SLOT, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
                        pa, b);
   }
-  static void finalize(const dev::PoolArgs<Node>& pa, int b, hipStream_t s) {
-    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, G::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa, b);
+  static void finalize(const dev::PoolArgs<Node>& pa, int b, int slot, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, G::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa, b, slot);
   }
   static int blocks_per_cu() {
     int n = 0;
@@ -78,8 +78,8 @@ struct PfspFrontTraits {
     hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, G::SLOT, G::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
                        pa, b);
   }
-  static void finalize(const dev::PoolArgs<Node>& pa, int b, hipStream_t s) {
-    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, G::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa, b);
+  static void finalize(const dev::PoolArgs<Node>& pa, int b, int slot, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, G::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa, b, slot);
   }
   static int blocks_per_cu() {
     int n = 0;

@@ -609,6 +609,10 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M, NJ>& a, FrontSme
     int nleaf = 0, inner = 0, o = 0, n = n0, cur = 0, lev0 = 0;
     uint4* const out = reinterpret_cast<uint4*>(bout + static_cast<size_t>(ch) * G::SLOT);
     const bool first = ch == static_cast<int>(blockIdx.x);
+    // wave priority falls with the level, as in front_local (ta014 -1.3 %,
+    // profiles/r5/fuse_prio_ab.txt); later chunks of a workgroup go last
+    if (first) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(0);
     if (wide) {
       uint32_t w[G::NW], r2[G::HW];
 #pragma unroll
@@ -654,6 +658,11 @@ __device__ inline void front_multi_level(const PfspFrontArgs<M, NJ>& a, FrontSme
     }
     if (first) front_stamp(a, 3);
     for (int lev = lev0; lev < L && n > 0; ++lev) {
+      if (first) {
+        if (lev == 0) __builtin_amdgcn_s_setprio(2);
+        else if (lev == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
       const bool last = lev == L - 1;
       const int nx = cur ^ 1;
       auto store = [&](int i, const uint32_t (&c)[G::NW], const uint32_t (&r)[G::HW]) {

@@ -576,12 +576,15 @@ __global__ __launch_bounds__(kBlock) void pool_weight_kernel(const Node* __restr
 // The control block is published to host-mapped memory with system-scope stores,
 // the sequence number last (release): the host polls that word instead of
 // waiting for the graph's completion signal (engine.hpp wait_oldest).
-// (b: the buffer the graph's last iteration wrote — graphs of 3k iterations end at phase 0
-// or 3: slot 0 either way, buffer b = phase & 1)
+// (b: the buffer the graph's last iteration wrote, s: the slot the next iteration would
+// read. Graphs of 3k iterations end at phase 0 or 3: slot 0. A learned first replay of
+// any length ends at slot s = K % 3; its slot is moved to slot 0, so the next replay
+// starts at phase 0 or 3 — the one whose buffer parity is b — engine.hpp launch_graph)
 template <class Node, int MAXCHUNKS>
-__global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa, int b) {
+__global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa, int b, int s) {
   __shared__ PoolSmem<MAXCHUNKS> ps;
-  const int n = pa.ctl->slot[0].nch;
+  const int n = pa.ctl->slot[s].nch;
+  if (s != 0 && threadIdx.x == 0) pa.ctl->slot[0] = pa.ctl->slot[s];
   const u64 seq = pa.ctl->seq + 1;
   int c = 0, l = 0, in = 0;
   {
@@ -613,11 +616,12 @@ __global__ __launch_bounds__(kBlock) void pool_finalize_kernel(PoolArgs<Node> pa
   constexpr int kPl = static_cast<int>(offsetof(PoolCtl, pend_leaves) / 4);
   constexpr int kPi = static_cast<int>(offsetof(PoolCtl, pend_internal) / 4);
   constexpr int kSeq = static_cast<int>(offsetof(PoolCtl, seq) / 4);
+  constexpr int kSlotW = static_cast<int>(sizeof(PoolCtl::Slot) / 4);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pa.ctl);
   uint32_t* dst = reinterpret_cast<uint32_t*>(pa.mirror);
   for (int i = threadIdx.x; i < static_cast<int>(sizeof(PoolCtl) / 4); i += kBlock) {
     if (i == kSeq || i == kSeq + 1) continue;
-    uint32_t x = src[i];
+    uint32_t x = src[(s != 0 && i < kSlotW) ? i + s * kSlotW : i];
     if (i == kPc) x = static_cast<uint32_t>(ct);
     if (i == kPc + 1) x = 0;
     if (i == kPl) x = static_cast<uint32_t>(lt);

@@ -24,8 +24,8 @@ struct QueensTraits {
     hipLaunchKernelGGL((dev::pool_flatten_kernel<Node, S::MAXCH, S::MAXCHUNKS>), dim3(grid), dim3(dev::kBlock), 0, s,
                        pa, b);
   }
-  static void finalize(const dev::PoolArgs<Node>& pa, int b, hipStream_t s) {
-    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, S::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa, b);
+  static void finalize(const dev::PoolArgs<Node>& pa, int b, int slot, hipStream_t s) {
+    hipLaunchKernelGGL((dev::pool_finalize_kernel<Node, S::MAXCHUNKS>), dim3(1), dim3(dev::kBlock), 0, s, pa, b, slot);
   }
   static int blocks_per_cu() {
     int n = 0;
