@@ -1,7 +1,9 @@
 """Iteration log of whole solves (TTS_ILOG, pool_device.hpp ilog_record): for every
 device iteration its start time, window, shape and the explored tree so far.
 
-    python scripts/ilog_probe.py [inst] [lb] [solves] [max_parents_log2]
+    python scripts/ilog_probe.py [inst] [lb] [solves] [max_parents_log2] [world]
+
+world > 1: rank 0's share of a world-way in-graph split (as scripts/share_solve_probe.py).
 
 Prints, per iteration of the last solve: the gap to the next iteration's start (its
 duration plus launch), the pool (S stack + C buffered children), the window B, the shape
@@ -27,9 +29,18 @@ solves = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 mp = int(sys.argv[4]) if len(sys.argv) > 4 else 19
 m = PfspModel(inst, lb)
 eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << mp, ring_bytes=4 << 30))
-for _ in range(solves):
-    r = solve_engine(m, eng, ub=1)
-print(f"ta{inst:03d} lb {lb}: tree {r.tree} sol {r.sol} best {r.best} elapsed {r.elapsed * 1e3:.3f} ms", flush=True)
+world = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+if world > 1:
+    for _ in range(solves):
+        nodes, t1, s1, best = m.warmup(m.initial_best(1), 25)
+        eng.set_split(0, world, 512 * world)
+        eng.begin(nodes, int(best))
+        eng.run()
+    print(f"ta{inst:03d} lb {lb}: rank 0 of {world}: tree {eng.stats()['tree']}", flush=True)
+else:
+    for _ in range(solves):
+        r = solve_engine(m, eng, ub=1)
+    print(f"ta{inst:03d} lb {lb}: tree {r.tree} sol {r.sol} best {r.best} elapsed {r.elapsed * 1e3:.3f} ms", flush=True)
 del eng
 import gc  # noqa: E402
 
