@@ -37,7 +37,9 @@ struct EngineConfig {
   // (measured on ta014, one MI355X: 3 / 4-level narrow chunks and 2 / 3-level wide ones
   // were 1-2 % / 2-19 % slower than two levels — the extra in-workgroup levels run
   // serially behind one another at ~6 us each, what a new iteration kernel also costs)
-  int deep_levels = 2;                   // fused iterations: at most this many tree levels (kernels that have them)
+  // fused iterations: at most this many tree levels (kernels that have them); 3 under the
+  // wave priority (ta014 0.188 -> 0.1855 ms, 4 slower; profiles/r5/ab2.txt)
+  int deep_levels = 3;
   int deep_per3 = 8;                     // ... 3 levels when a workgroup takes at most this many parents
   int deep_per4 = 2;                     // ... 4 levels when a workgroup takes at most this many parents
   // dynamic local DFS iterations (front kernel): time budget of one iteration in us
