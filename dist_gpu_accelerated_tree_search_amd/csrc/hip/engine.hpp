@@ -496,15 +496,19 @@ class DeviceEngine final : public IEngine, public DeviceResource {
       if (all == 0) {
         // the tree is done: the next solve's first replay gets this solve's iteration
         // count, so it ends without empty iterations (ta014: 2 empty launches of ~5 us
-        // each when rounded up to whole phases). Dynamic iterations keep whole phases:
-        // their control sets rotate with the slot (dyn_zero_next)
+        // each when rounded up to whole phases). Exact only when two solves in a row took
+        // the same count (a count that varies — rank shares, -u 0 — keeps the fewer
+        // whole-phase lengths, each a graph captured on first use); dynamic iterations
+        // keep whole phases: their control sets rotate with the slot (dyn_zero_next)
         const dev::u64 it = h_ctl_->iters;
+        const bool stable = static_cast<int>(it) == last_iters_;
+        last_iters_ = static_cast<int>(it);
 #ifdef TTS_LEARN_ROUND  // A/B builds: whole phases
         const bool exact = false;
 #else
         const bool exact = args_.pool.dyn == nullptr;
 #endif
-        learned_k_ = (it >= 1 && it <= 48) ? static_cast<int>(exact ? it : (it + 2) / 3 * 3) : 0;
+        learned_k_ = (it >= 1 && it <= 48) ? static_cast<int>(exact && stable ? it : (it + 2) / 3 * 3) : 0;
         break;
       }
       if (all < stop_below) break;
@@ -1305,6 +1309,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   int phase_ = 0;         // t of the next iteration: 0 or 3
   bool learn_first_ = true;  // first replay after begin() = the previous solve's iterations (TTS_LEARN_FIRST=0: off)
   int learned_k_ = 0;     // ... (0: unknown)
+  int last_iters_ = -1;   // the previous finished solve's iteration count
   std::vector<void*> owned_;
   hipEvent_t ev_ahead_ = nullptr;  // after the latest export_ahead copy (transfer stream)
   bool ahead_copy_ = false;

@@ -1,6 +1,6 @@
 set -o pipefail
 # 2 ranks sharing GPU 0 (gloo transfers), headline + ta021 extra with per-rank idle / load-balance clocks
-out=gpurun_out/r5n2; mkdir -p $out
+out=${N2OUT:-gpurun_out/r5n2}; mkdir -p $out
 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --comm gloo --device 0 --extras ta021 > $out/bench_n2.json 2> $out/bench_n2.err || { tail -30 $out/bench_n2.err; exit 1; }
 python3 -c "
 import json;d=json.load(open('$out/bench_n2.json'))
