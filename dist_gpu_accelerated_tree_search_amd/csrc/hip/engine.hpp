@@ -149,8 +149,6 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     pa.local_min = cfg_.local_min >= 0 ? cfg_.local_min
                    : (cfg_.max_parents >= resident * Traits::kParentsPerChunk ? Traits::kLocalMin : 0);
     if (const char* f = std::getenv("TTS_LOCAL_MIN")) pa.local_min = std::max(0, std::atoi(f));
-    pa.local_cap = 0;
-    if (const char* f = std::getenv("TTS_LOCAL_CAP")) pa.local_cap = std::max(0, std::atoi(f));
     // local DFS windows dealt strided (chunk ch takes window parents ch, ch + nchunks, ...)
     // below a backlog (pool_begin): consecutive window nodes are one previous chunk's stack,
     // siblings with alike survivor counts, so contiguous dealing handed some workgroups all

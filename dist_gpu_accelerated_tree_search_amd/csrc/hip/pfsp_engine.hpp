@@ -596,7 +596,6 @@ std::vector<double> pfsp_front_time_t(const PfspInstance& in, int lb, const void
   pa.fuse_max = cfg.fuse_max;
   pa.local_steps = std::min(cfg.local_steps, G::LT);
   pa.local_min = std::max(0, cfg.local_min);
-  pa.local_cap = 0;
   pa.local_stride = 0;
   pa.local_wide_steps = 0;
   if (const char* f = std::getenv("TTS_LOCAL_STRIDE")) pa.local_stride = std::atoi(f);

@@ -791,7 +791,7 @@ __device__ inline void front_local(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, N
       // will another step run? then the children it pops (the last min(top, kBlock)
       // pushed) stay in LDS and skip the slot region's store / load round trip
       const int tnew = top + tot;
-      const bool more = s + 1 < v.steps && tnew > 0 && !(tnew + kBlock * G::NJ > G::SLOT || tnew > v.cap);
+      const bool more = s + 1 < v.steps && tnew > 0 && tnew + kBlock * G::NJ <= G::SLOT;
       nst = more ? min(tot, min(tnew, kBlock)) : 0;
       const int lo = tot - nst;
       uint4* const dst = reinterpret_cast<uint4*>(stk + top);

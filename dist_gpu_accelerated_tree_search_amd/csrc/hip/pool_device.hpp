@@ -107,7 +107,6 @@ struct PoolArgs {
   int fuse_max;     // two-level iterations for windows of at most this many parents (0: off)
   int local_steps;  // > 1: local DFS iterations of up to this many steps per chunk (kernels that have them)
   int local_min;    // wide local DFS when the pool holds at least this many parents (0: 4 grid windows)
-  int local_cap;    // > 0: a local DFS chunk takes no further step once its stack holds more than this
   int local_stride;    // local DFS chunks take strided window parents (ch, ch + nchunks, ...)
   int local_wide_steps;  // > 0: steps of a strided local window of at least 160 parents per workgroup
   // multi-level iterations (kernels with LMAX > 2): a fused window of at most deep_per[0]
@@ -244,7 +243,6 @@ struct IterView {
   bool stride;        // local DFS: chunk ch takes window parents ch, ch + nchunks, ... (pa.local_stride)
   int bp;             // window parents per chunk
   int steps;          // local DFS: steps per chunk at most
-  int cap;            // local DFS: no further step once the stack holds more than this
   int srank, sworld;
   bool armed;         // a rank split is pending: the pool is replicated on every rank
   bool dyn;           // dynamic local DFS (front_dyn): chunk ch = workgroup ch, queue chunks after them
@@ -313,7 +311,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     v.levels = 1;
     if (DYN) dyn_zero_next(pa.dyn, t);
     v.bp = BP;
-    v.steps = v.cap = 0;
+    v.steps = 0;
     v.srank = v.sworld = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       ctl->slot[s_out].stack = 0;
@@ -351,7 +349,6 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // vs 4 steps 0.219 ms; under the step priority 3 / 4 / 5 steps 0.206 / 0.210 / 0.215 ms,
   // profiles/r5/steps_ab.txt)
   if (v.stride && pa.local_wide_steps > 0 && min(v.B, full) >= 160ull * gridDim.x) v.steps = pa.local_wide_steps;
-  v.cap = pa.local_cap > 0 ? pa.local_cap : 0x7fffffff;
   // dynamic local DFS: every workgroup owns its chunk (the window dealt strided over the
   // grid) and steps until the time budget, sharing work through the queue slots
   v.dyn = DYN && v.local && pa.dyn != nullptr && pa.dyn_ticks > 0 && pa.dyn_q > 0 &&
