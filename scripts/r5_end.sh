@@ -1,0 +1,11 @@
+set -o pipefail
+out=gpurun_out/r5end; mkdir -p $out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.txt 2>&1 || { tail -20 $out/smoke.txt; exit 1; }
+tail -1 $out/smoke.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $out/gpu_tests.txt 2>&1 || { tail -30 $out/gpu_tests.txt; exit 1; }
+tail -1 $out/gpu_tests.txt
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $out/bench_n1.json 2> $out/bench_n1.err || { tail -30 $out/bench_n1.err; exit 1; }
+python3 -c "
+import json;d=json.load(open('$out/bench_n1.json'))
+print('headline', round(d['ms_per_step'],4), 'ms', round(d['value']/1e9,3), 'G nodes/s')
+for k,e in d.get('extras',{}).items(): print(k, {x: e.get(x) for x in ('seconds','nodes_per_s','golden_ok')})"
