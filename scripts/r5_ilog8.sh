@@ -1,5 +1,5 @@
 set -o pipefail
-out=gpurun_out/r5ilog8; mkdir -p $out
+out=${ILOG_OUT:-gpurun_out/r5ilog8}; mkdir -p $out
 mod=$(ls dist_gpu_accelerated_tree_search_amd/_tts_hip*.so)
 cp build/ab/ilog/$(basename $mod) $mod
 for w in 1 8; do
