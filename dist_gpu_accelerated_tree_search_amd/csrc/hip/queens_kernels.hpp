@@ -183,7 +183,16 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
   if (fin_from != INT_MAX) {
     // the subtrees of this workgroup's finishing parents (read again from the window):
     // no barrier between them, so a wave with a deep subtree holds up no other wave
+    // wave priority falls with the chunks a workgroup has finished: the CU's late-dispatched
+    // workgroups catch up instead of trailing (N=17 170 -> 174 G nodes/s,
+    // profiles/r5/queens_prio_ab.txt; the same age-priority effect as front_local's)
+    int k = 0;
     for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
+      if (k == 0) __builtin_amdgcn_s_setprio(3);
+      else if (k == 1) __builtin_amdgcn_s_setprio(2);
+      else if (k == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+      ++k;
       const u64 gi = static_cast<u64>(ch) * S::BP + tid;
       if (gi < v.B) {
         const QueensNode nd = *pool_parent<QueensNode, S::MAXCH, S::MAXCHUNKS>(pa, v, t, gi, sm.pool);
