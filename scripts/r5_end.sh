@@ -1,5 +1,5 @@
 set -o pipefail
-out=gpurun_out/r5end; mkdir -p $out
+out=${END_OUT:-gpurun_out/r5end}; mkdir -p $out
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.txt 2>&1 || { tail -20 $out/smoke.txt; exit 1; }
 tail -1 $out/smoke.txt
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $out/gpu_tests.txt 2>&1 || { tail -30 $out/gpu_tests.txt; exit 1; }
