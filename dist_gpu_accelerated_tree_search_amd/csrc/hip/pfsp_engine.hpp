@@ -85,7 +85,7 @@ struct PfspFrontTraits {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_front_kernel<M, NJ>, dev::kBlock, 0) != hipSuccess)
       return 1;
-    return std::min(n, G::WAVES);  // FrontGeom::WAVES: the API over-reports by one
+    return std::min(n, G::GRID_WGS);  // FrontGeom::GRID_WGS (the API over-reports by one)
   }
 };
 

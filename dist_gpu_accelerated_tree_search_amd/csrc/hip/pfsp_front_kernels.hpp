@@ -64,6 +64,10 @@ struct FrontGeom {
   // lifetime late, +1.3 us per wide iteration, +4 us per multi-level one)
   // (50-job nodes: 16 words for 20 machines, 12 for 10: 5 waves up to 10 machines)
   static constexpr int WAVES = NJ > 20 ? (M <= 5 ? 6 : M <= 10 ? 5 : 4) : (M <= 10 ? 6 : 4);
+  // resident workgroups per CU the engine's grid is sized for: under the step priority one
+  // below the register budget's 6 for 20-job, <= 10-machine instances (ta014 0.1840 ->
+  // 0.1822 ms, 2/4/8-way shares -2..-4 %, ta008 3 engines +8 %; profiles/r5/grid_ab.txt)
+  static constexpr int GRID_WGS = NJ > 20 ? WAVES : (M <= 10 ? 5 : 4);
   // probe records (tests): {job | kind << 8, lb, parent words, parent remain}
   static constexpr int DBGW = (2 + NW + (M + 1) / 2 + 3) / 4 * 4;
   static constexpr int HW = (M + 1) / 2;  // packed u16 pairs of a p row / a remain
@@ -1230,8 +1234,8 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
 //
 // Occupancy: the iterations are latency-bound (the per-child chain, LDS row reads), so
 // the register budget is capped for more resident waves: 6 per SIMD up to 10 machines,
-// 4 for 20 (f, remain and a p row stay in registers without scratch); FrontGeom::WAVES
-// sizes the engine's grid to match. (Compiled for 7 — 94 SGPRs, 72 spilled to VGPR
+// 4 for 20 (f, remain and a p row stay in registers without scratch); the engine's grid
+// holds FrontGeom::GRID_WGS workgroups per CU (5 of the 6 up to 10 machines). (Compiled for 7 — 94 SGPRs, 72 spilled to VGPR
 // lanes — the headline was 3 % slower than at 6.)
 template <int M, int NJ = 20>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FrontGeom<M, NJ>::WAVES)))
