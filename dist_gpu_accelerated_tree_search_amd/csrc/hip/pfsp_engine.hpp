@@ -50,7 +50,10 @@ struct PfspTraits {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::pfsp_expand_kernel<NJ, M, LBK>, dev::kBlock, 0) !=
         hipSuccess)
       return 1;
-    return dev::resident_blocks(n);  // 106 SGPRs: 6 resident per CU
+    // 106 SGPRs: 6 resident per CU. The packed LB2 walks of 50+-job instances run on 3 of
+    // their 4 (LDS-bound) resident workgroups: fewer walks contend for the record lines
+    // (ta056 0.1748 -> 0.1773 G nodes/s, 2 per CU 0.1765; profiles/r5/grid_ab.txt)
+    return dev::resident_blocks(n, (LBK == 5 && NJ >= 50) ? 3 : dev::kSgprResidentCap);
   }
 };
 
