@@ -31,7 +31,9 @@ struct QueensTraits {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dev::queens_expand_kernel, dev::kBlock, 0) != hipSuccess)
       return 1;
-    return dev::resident_blocks(n);  // 106 SGPRs: 6 resident per CU
+    // 106 SGPRs allow 6 resident per CU; the grid takes 5 (N=17 47.1 -> 46.0 ms, 4 and 8
+    // slower; profiles/r5/grid_ab.txt)
+    return dev::resident_blocks(n, 5);
   }
 };
 
