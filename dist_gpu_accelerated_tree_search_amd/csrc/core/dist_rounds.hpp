@@ -329,6 +329,11 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
     }
   } no_overlap{e, overlap};
   unsigned long long overlapped = 0;
+  // while some rank starves, slices end without a replay in flight: a donor mid-replay can
+  // only export what the replay does not hold, and a skewed start then stayed unbalanced
+  // (4 ranks, all work on one: per-rank trees max/mean 1.2-1.6 overlapped, 1.03 not;
+  // profiles/r5/skew_overlap.txt); once every rank has work, rounds overlap again
+  bool ov_now = overlap;
 
   // status record: pool size, incumbent, split pending, time up, exportable now
   constexpr int kRec = 5;
@@ -454,6 +459,10 @@ inline DistOutcome run_dist_rounds(IEngine& e, RoundControl& ctl, const DistOpti
       slice = o.slice_min;
     } else {
       slice = std::min(o.slice_max, slice * 2);
+    }
+    if (overlap && (!starving || replicated) != ov_now) {
+      ov_now = !ov_now;
+      e.set_overlap(ov_now);
     }
     if (size == 0) t_term += secs(t1, clock::now());
     t_comm += secs(t1, clock::now());
