@@ -34,8 +34,8 @@ from .utils import report
 INT_MAX = 2**31 - 1
 
 
-def _pfsp_parser() -> argparse.ArgumentParser:
-    ap = argparse.ArgumentParser(prog="pfsp", description="PFSP Branch-and-Bound (Taillard instances)")
+def _pfsp_parser(cls=argparse.ArgumentParser) -> argparse.ArgumentParser:
+    ap = cls(prog="pfsp", description="PFSP Branch-and-Bound (Taillard instances)")
     ap.add_argument("-i", "--inst", type=int, default=14)
     ap.add_argument("-l", "--lb", type=int, default=1)
     ap.add_argument("-u", "--ub", type=int, default=1)
@@ -98,6 +98,10 @@ def _validate_pfsp(a) -> None:
         fail("Error: unsupported distributed dynamic load balancing option")
     if not 0 < a.perc <= 100:
         fail("Error: unsupported WS percentage for popFrontBulkFree")
+    if a.device is not None and a.comm != "gloo":
+        # RCCL builds one communicator per rank on that rank's own GPU (LOCAL_RANK) and
+        # refuses two ranks on one device: ranks pinned to one GPU need the gloo transport
+        fail("Error: --device puts every rank on one GPU; use it with --comm gloo")
 
 
 def _steal_cap(a) -> int:
@@ -211,8 +215,9 @@ def pfsp_main(argv: list[str]) -> int:
             return 0
     else:
         from .ops import gpu_count
-        from .parallel.launch import spawn_local
+        from .parallel.launch import spawn_local, warm_forkserver
 
+        warm_forkserver()  # before gpu_count: the ranks never come from a GPU-initialised process
         if (a.D > gpu_count()) if a.device is None else (a.device >= gpu_count()):
             print("Execution Terminated. More GPU devices requested than the ones available")
             return 1
@@ -249,8 +254,8 @@ def _json(a, model, r, n_gpus) -> None:
                                           "workers": [asdict(w) for w in r.workers]})
 
 
-def nqueens_main(argv: list[str]) -> int:
-    ap = argparse.ArgumentParser(prog="nqueens", description="N-Queens backtracking")
+def _nqueens_parser(cls=argparse.ArgumentParser) -> argparse.ArgumentParser:
+    ap = cls(prog="nqueens", description="N-Queens backtracking")
     ap.add_argument("-N", type=int, default=14)
     ap.add_argument("-g", type=int, default=1)
     ap.add_argument("-m", type=int, default=25)
@@ -261,7 +266,11 @@ def nqueens_main(argv: list[str]) -> int:
     # MI355X with 2 (profiles/r3/queens/streams_probe.txt)
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--stream-split", type=int, default=512)
-    a = ap.parse_args(argv)
+    return ap
+
+
+def nqueens_main(argv: list[str]) -> int:
+    a = _nqueens_parser().parse_args(argv)
     for name, v in (("N", a.N), ("g", a.g), ("m", a.m)):
         if v < 1:
             sys.stderr.write(f"Error: {name} must be a positive integer.\n")
@@ -298,8 +307,9 @@ def nqueens_main(argv: list[str]) -> int:
         if res["rank"] != 0:
             return 0
     else:
-        from .parallel.launch import spawn_local
+        from .parallel.launch import spawn_local, warm_forkserver
 
+        warm_forkserver()
         res = spawn_local(a.D, solve_rank, (spec,))[0]
     print(report.queens_settings(a.N, a.g, f"Multi-GPU C++/HIP+RCCL ({res['world']} GPUs)"))
     print(report.phase("Search on GPU completed", res["tree"], res["sol"], res["t_search"]))
@@ -308,32 +318,27 @@ def nqueens_main(argv: list[str]) -> int:
     return 0
 
 
+class _QuietParser(argparse.ArgumentParser):
+    def error(self, message):  # parse errors are reported by the real parse in *_main
+        raise ValueError(message)
+
+
 def _spawn_planned(argv: list[str]) -> bool:
-    """Will this command start one process per GPU itself (spawn_local)? That is -D N > 1
-    outside torchrun, for N-Queens always and for PFSP with -C 0 and no single-process
-    option. Parsed leniently: a wrong guess only costs (or skips) an early forkserver."""
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or len(argv) < 2:
+    """Will this command start one process per GPU itself (spawn_local)? Decided with the
+    same parsers and the same routing tests as pfsp_main / nqueens_main (so `-D2`,
+    `--D=3` and abbreviated long options count), before anything touches HIP."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or not argv:
         return False
-
-    def opt(short: str, long: str, default: str) -> str:
-        v = default
-        for i, x in enumerate(argv):
-            if x in (short, long) and i + 1 < len(argv):
-                v = argv[i + 1]
-            elif x.startswith(long + "="):
-                v = x.split("=", 1)[1]
-        return v
-
     try:
-        D = int(opt("-D", "--D", "1"))
-        C = int(opt("-C", "--C", "1"))
-    except ValueError:
+        if argv[0] == "nqueens":
+            a = _nqueens_parser(_QuietParser).parse_args(argv[1:])
+            return a.D > 1
+        a = _pfsp_parser(_QuietParser).parse_args(argv[1:])
+    except (ValueError, SystemExit):
         return False
-    if D <= 1:
-        return False
-    if argv[0] == "nqueens":
-        return True
-    return C == 0 and "--single-process" not in argv and not any(x.startswith("--gpus-list") for x in argv)
+    # pfsp_main: D == 0 is CPU only; C == 1 / --single-process / --gpus-list is the native
+    # runner; D == 1 is the single-GPU path; every other D goes through spawn_local
+    return a.D > 1 and not (a.C == 1 or a.single_process or a.gpus_list)
 
 
 def main(argv: list[str] | None = None) -> int:

@@ -11,9 +11,11 @@ from __future__ import annotations
 import multiprocessing as mp
 import os
 import socket
+import sys
 import traceback
 
 _CTX = None
+_WARM = False
 
 
 def _ctx():
@@ -26,10 +28,27 @@ def _ctx():
 
 def warm_forkserver() -> None:
     """Start the forkserver now (call before any GPU use in this process)."""
+    global _WARM
+    if _WARM:
+        return
     ctx = _ctx()
     p = ctx.Process(target=_noop)
     p.start()
     p.join()
+    _WARM = True
+
+
+def hip_touched() -> bool:
+    """True once this process may have initialised HIP: torch's lazy CUDA/HIP init ran, or
+    the gfx950 extension was loaded (its engines make HIP calls)."""
+    torch = sys.modules.get("torch")
+    try:
+        if torch is not None and torch.cuda.is_initialized():
+            return True
+    except Exception:  # pragma: no cover - torch without a cuda module
+        pass
+    ops = sys.modules.get("dist_gpu_accelerated_tree_search_amd.ops")
+    return ops is not None and getattr(ops, "_hip_mod", None) is not None
 
 
 def _noop():
@@ -53,7 +72,15 @@ def _entry(rank, world, port, fn, args, q, env):
 
 
 def spawn_local(world: int, fn, args=(), timeout: float = 600.0, env: dict | None = None) -> list:
-    """Run fn(*args) in `world` ranks; returns the per-rank results (rank order)."""
+    """Run fn(*args) in `world` ranks; returns the per-rank results (rank order).
+
+    Refuses to start the forkserver from a process that may have initialised HIP: the
+    forkserver is a fork+exec, and exec from a GPU-initialised process is forbidden
+    (call warm_forkserver() first, as the CLI and the test session do)."""
+    if not _WARM and hip_touched():
+        raise RuntimeError("spawn_local: the rank forkserver was not started before this process used HIP; "
+                           "call parallel.launch.warm_forkserver() before any GPU call")
+    warm_forkserver()
     ctx = _ctx()
     q = ctx.Queue()
     port = free_port()

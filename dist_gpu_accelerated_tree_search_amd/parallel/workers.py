@@ -22,6 +22,8 @@ def solve_rank(spec: dict) -> dict:
     """Solve spec's problem cooperatively on all ranks of the current process group."""
     backend = spec.get("backend", "gpu")
     # comm on the GPU (RCCL) unless asked for gloo, e.g. several ranks sharing one GPU
+    if backend == "gpu" and "device" in spec and spec.get("comm", "nccl") == "nccl":
+        raise ValueError("spec['device'] puts ranks on one GPU: RCCL needs one GPU per rank, use comm='gloo'")
     comm = Comm(use_gpu=(backend == "gpu" and spec.get("comm", "nccl") == "nccl"))
     try:
         model = build_model(spec)

@@ -17,6 +17,11 @@ from dist_gpu_accelerated_tree_search_amd.parallel import launch
     (["pfsp", "--D=3", "--C=0"], True),
     (["nqueens", "-N", "12", "-D", "2"], True),
     (["nqueens", "-N", "12"], False),
+    (["pfsp", "-D2", "-C0"], True),                    # joined short options
+    (["pfsp", "-D", "2", "-C", "2"], True),            # same routing test as pfsp_main (C != 1)
+    (["pfsp", "-D", "3", "-C", "0", "--single"], False),  # abbreviated --single-process
+    (["pfsp", "-D", "0", "-C", "4"], False),           # CPU only
+    (["nqueens", "-D3"], True),
 ])
 def test_spawn_planned(argv, want, monkeypatch):
     monkeypatch.delenv("WORLD_SIZE", raising=False)
@@ -41,4 +46,24 @@ def test_forkserver_starts_before_any_gpu_call(monkeypatch, capsys):
     rc = cli.main(["pfsp", "-i", "14", "-D", "2", "-C", "0", "--no-csv"])
     assert rc == 1
     assert "More GPU devices requested" in capsys.readouterr().out
-    assert calls == ["forkserver", "gpu_count"], calls
+    assert calls[0] == "forkserver" and calls[-1] == "gpu_count" and calls.count("gpu_count") == 1, calls
+
+
+def test_spawn_local_refuses_forkserver_after_hip(monkeypatch):
+    monkeypatch.setattr(launch, "_WARM", False)
+    monkeypatch.setattr(launch, "hip_touched", lambda: True)
+    with pytest.raises(RuntimeError, match="forkserver"):
+        launch.spawn_local(2, print)
+
+
+def test_device_needs_gloo(capsys):
+    with pytest.raises(SystemExit):
+        cli.main(["pfsp", "-D", "2", "-C", "0", "--device", "0", "--no-csv"])
+    assert "--comm gloo" in capsys.readouterr().err
+
+
+def test_rank_spec_device_needs_gloo():
+    from dist_gpu_accelerated_tree_search_amd.parallel.workers import solve_rank
+
+    with pytest.raises(ValueError, match="gloo"):
+        solve_rank({"problem": "pfsp", "backend": "gpu", "device": 0, "comm": "nccl"})
