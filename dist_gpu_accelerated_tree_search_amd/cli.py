@@ -62,6 +62,9 @@ def _pfsp_parser(cls=argparse.ArgumentParser) -> argparse.ArgumentParser:
                     help="one process per GPU: node transfers over RCCL (default) or gloo (ranks may share a GPU)")
     ap.add_argument("--device", type=int, default=None,
                     help="one process per GPU: put every rank on this device (tests; use with --comm gloo)")
+    ap.add_argument("--heuristic-ub", action="store_true",
+                    help="-u 0: start from a heuristic incumbent (LB1 beam dive + NEH) instead of +inf; the "
+                         "explored tree is then not the reference's -u 0 quantity (recorded as initial_ub)")
     ap.add_argument("--json", default=None, help="append a JSON run record to this file")
     ap.add_argument("--csv-dir", default=".", help="directory of the CSV statistics files")
     ap.add_argument("--no-csv", action="store_true")
@@ -146,7 +149,8 @@ def _pfsp_single_process(a, model) -> int:
         print("Execution Terminated. More GPU devices requested than the ones available")
         return 1
     threads = _cpu_worker_threads(len(devices), a.streams) if a.C == 1 else 0
-    print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, a.D, a.C, a.ws, 1, a.L, 2))
+    print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, a.D, a.C, a.ws, 1, a.L, 2,
+                               _init_ub(a, model)))
     opts = EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * 2**30), cpu_batch=a.T,
                          cpu_threads=max(1, threads), streams=max(1, a.streams))
     r = solve_workers(model, devices=tuple(devices), cpu_threads=threads, ub=a.ub, m=a.m, steal_cap=_steal_cap(a),
@@ -166,6 +170,8 @@ def _pfsp_single_process(a, model) -> int:
 def pfsp_main(argv: list[str]) -> int:
     a = _pfsp_parser().parse_args(argv)
     _validate_pfsp(a)
+    if a.heuristic_ub:
+        os.environ.setdefault("TTS_DIVE", "32")  # models.pfsp.PfspModel.search_best
     from .models.pfsp import EngineOptions, PfspModel
     from .search import solve_cpu, solve_engine
 
@@ -189,7 +195,8 @@ def pfsp_main(argv: list[str]) -> int:
         return _pfsp_single_process(a, model)
 
     if a.D == 1 and world_env == 1:
-        print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, 1, a.C, a.ws, 1, a.L, 2))
+        print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, 1, a.C, a.ws, 1, a.L, 2,
+                                   _init_ub(a, model)))
         eng = model.make_engine("gpu", 0, EngineOptions(max_parents=a.max_parents, ring_bytes=int(a.ring_gb * 2**30),
                                                         streams=max(1, a.streams)))
         r = solve_engine(model, eng, ub=a.ub, m=a.m, verbose=True)
@@ -207,6 +214,8 @@ def pfsp_main(argv: list[str]) -> int:
     from .parallel.workers import solve_rank
 
     spec = _rank_spec(a, world_env if world_env > 1 else a.D)
+    if a.heuristic_ub:
+        spec["heuristic_ub"] = True
     if world_env == 1:
         spec["dist"]["cpu_workers"] = 0  # spawned ranks: -C 0 (with -C 1 this was the native runner)
     if world_env > 1:  # already under torchrun
@@ -223,7 +232,8 @@ def pfsp_main(argv: list[str]) -> int:
             return 1
         res = spawn_local(a.D, solve_rank, (spec,))[0]
     D = res["world"]
-    print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, D, a.C, a.ws, 1, a.L, 2))
+    print(report.pfsp_settings(a.inst, model.machines, model.jobs, a.ub, a.lb, D, a.C, a.ws, 1, a.L, 2,
+                               _init_ub(a, model)))
     print(report.phase("Search on Parallel GPU completed", res["tree"], res["sol"], res["t_search"]))
     print("\nExploration terminated.")
     print(report.pfsp_results(res["best"], res["tree"], res["sol"], res["elapsed"]))
@@ -241,7 +251,8 @@ def pfsp_main(argv: list[str]) -> int:
         report.write_json_record(a.json, {**model.describe(), "n_gpus": D, "tree": res["tree"], "sol": res["sol"],
                                            "best": res["best"], "elapsed": res["elapsed"],
                                            "nodes_per_sec": res["tree"] / max(res["elapsed"], 1e-12),
-                                           "rounds": res["extra"]["rounds"], "workers": res["workers"]})
+                                           "rounds": res["extra"]["rounds"], "workers": res["workers"],
+                                           "initial_ub": _init_ub(a, model)})
     return 0
 
 
@@ -251,7 +262,17 @@ def _json(a, model, r, n_gpus) -> None:
 
         report.write_json_record(a.json, {**model.describe(), "n_gpus": n_gpus, "tree": r.tree, "sol": r.sol,
                                           "best": r.best, "elapsed": r.elapsed, "nodes_per_sec": r.nodes_per_sec,
-                                          "workers": [asdict(w) for w in r.workers]})
+                                          "workers": [asdict(w) for w in r.workers], "initial_ub": _init_ub(a, model)})
+
+
+def _init_ub(a, model) -> int | None:
+    """The incumbent the device search starts from: the best-known makespan with -u 1,
+    None (+inf) with -u 0, the heuristic schedule's makespan with --heuristic-ub."""
+    if a.ub == 1:
+        return int(model.best_known)
+    if getattr(a, "heuristic_ub", False) and a.D >= 1:
+        return int(model.search_best(0))
+    return None
 
 
 def _nqueens_parser(cls=argparse.ArgumentParser) -> argparse.ArgumentParser:

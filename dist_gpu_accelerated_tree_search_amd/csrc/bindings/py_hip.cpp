@@ -25,9 +25,12 @@ namespace {
 using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 
 EngineConfig make_cfg(int device, size_t max_parents, size_t ring_bytes, int iters_small, int iters_large,
-                      bool use_graphs, uintptr_t stream, int iters_first, int dyn_us = 0) {
+                      bool use_graphs, uintptr_t stream, int iters_first, int dyn_us = 0, int dive_window = 0,
+                      int dive_shift = 2) {
   EngineConfig c;
   c.dyn_us = dyn_us;
+  c.dive_window = dive_window;
+  c.dive_shift = dive_shift;
   c.device = device;
   c.max_parents = max_parents;
   c.ring_bytes = ring_bytes;
@@ -103,6 +106,7 @@ PYBIND11_MODULE(_tts_hip, m) {
       .def_property_readonly("bytes_sent", &RcclTransport::bytes_sent)
       .def_property_readonly("bytes_recv", &RcclTransport::bytes_recv)
       .def_property_readonly("collectives", &RcclTransport::collectives)
+      .def_property("timeout_s", &RcclTransport::timeout_s, &RcclTransport::set_timeout_s)
       .def(
           "allgather_i64",
           [](RcclTransport& t, std::vector<int64_t> v, IEngine& e) {
@@ -194,17 +198,17 @@ PYBIND11_MODULE(_tts_hip, m) {
       "make_pfsp_engine",
       [](int jobs, int machines, std::vector<int> p, int lb, int device, size_t max_parents, size_t ring_bytes,
          int iters_small, int iters_large, bool use_graphs, uintptr_t stream, int taillard_id, int iters_first,
-         int dyn_us) {
+         int dyn_us, int dive_window, int dive_shift) {
         const PfspInstance in = make_instance(jobs, machines, std::move(p), taillard_id);
         py::gil_scoped_release nogil;
         return make_pfsp_engine(in, lb,
                                 make_cfg(device, max_parents, ring_bytes, iters_small, iters_large, use_graphs, stream,
-                                         iters_first, dyn_us));
+                                         iters_first, dyn_us, dive_window, dive_shift));
       },
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("device") = 0,
       py::arg("max_parents") = size_t(1) << 18, py::arg("ring_bytes") = size_t(16) << 30, py::arg("iters_small") = 6,
       py::arg("iters_large") = 48, py::arg("use_graphs") = true, py::arg("stream") = 0, py::arg("taillard_id") = 0,
-      py::arg("iters_first") = 18, py::arg("dyn_us") = 0);
+      py::arg("iters_first") = 18, py::arg("dyn_us") = 0, py::arg("dive_window") = 0, py::arg("dive_shift") = 2);
 
   m.def(
       "make_queens_engine",

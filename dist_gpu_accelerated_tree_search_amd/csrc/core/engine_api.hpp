@@ -46,6 +46,11 @@ struct EngineConfig {
   // (0: fixed-step local iterations)
   int dyn_us = 0;
   int wide_levels = 1;                   // wide windows (<= one parent per thread): levels per iteration (< 2: off)
+  // -u 0 dive (pool_device.hpp Slot::cap): a solve begun without an incumbent expands at
+  // most this many parents per iteration until its first leaf, then the cap grows by
+  // 2^dive_shift per iteration (0: off — N-Queens, which has no incumbent)
+  int dive_window = 0;
+  int dive_shift = 2;
   bool use_graphs = true;
   uintptr_t external_stream = 0;         // run on this stream when non-zero
 };

@@ -107,6 +107,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&xfer_, hipStreamNonBlocking));
     std::memset(h_ctl_, 0, sizeof(dev::PoolCtl));
     h_ctl_->best.v = 0x7fffffff;
+    h_ctl_->dive_shift = cfg_.dive_shift;
     if (cfg_.external_stream) {
       stream_ = reinterpret_cast<hipStream_t>(cfg_.external_stream);
     } else {
@@ -631,6 +632,9 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     h_ctl_->split_rank = arm_rank_;
     h_ctl_->split_min = arm_min_;
     for (int i = 0; i < 3; ++i) h_ctl_->slot[i].sdone = 0;
+    // -u 0 (no incumbent yet): dive to the first leaves through a narrow window
+    h_ctl_->slot[0].cap = (best == 0x7fffffff && cfg_.dive_window > 0) ? static_cast<unsigned>(cfg_.dive_window) : 0u;
+    h_ctl_->slot[0].cpad = 0x7fffffffu;
     const bool armed = arm_world_ > 1;
     arm_world_ = 0;
     if (armed && n > cfg_.max_parents)

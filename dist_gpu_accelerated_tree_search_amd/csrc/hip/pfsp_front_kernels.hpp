@@ -854,14 +854,19 @@ __device__ inline int dyn_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELA
 __device__ inline unsigned dyn_ldu(unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ inline void dyn_stu(unsigned* p, unsigned x) {
-  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ inline int dyn_add(int* p, int x) {
   return __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Slot hand-offs follow the memory model, not the hardware's in-order behaviour: the
+// publishing store (full / free) is a release by the workgroup's thread 0 after the
+// barrier that ends every wave's payload accesses, the claiming CAS an acquire before the
+// barrier that starts the claimer's payload reads (barrier + agent-scope release /
+// acquire are cumulative).
+__device__ inline void dyn_stu_rel(unsigned* p, unsigned x) {
+  __hip_atomic_store(p, x, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ inline bool dyn_cas(unsigned* p, unsigned expect, unsigned want) {
-  return __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+  return __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1113,7 +1118,7 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload is complete
       __syncthreads();
       if (tid == 0) {
-        dyn_stu(&pa.dyn[t % 3].st[qslot(dslot)], 2u | (static_cast<unsigned>(n) << 8));
+        dyn_stu_rel(&pa.dyn[t % 3].st[qslot(dslot)], 2u | (static_cast<unsigned>(n) << 8));
         dyn_add(&part().avail, 1);
         sm.dyn.pad += 1 << 10;
       }
@@ -1162,7 +1167,7 @@ __device__ inline void front_dyn(const PfspFrontArgs<M, NJ>& a, FrontSmem<M, NJ>
       const int q = r & 0xffff, n = r >> 16;
       dyn_copy<M, NJ>(region(q), stk, n, 2);
       __syncthreads();  // the block is read (and the copy visible to the next pops)
-      if (tid == 0) dyn_stu(&pa.dyn[t % 3].st[qslot(q)], 0u);
+      if (tid == 0) dyn_stu_rel(&pa.dyn[t % 3].st[qslot(q)], 0u);
       base = 0;
       top = n;
       nst = 0;

@@ -36,6 +36,13 @@ struct PoolCtl {
     u64 stack;  // ring occupancy at the start of iteration t
     int nch;    // chunks written by iteration t-1 into buffer t%2
     int sdone;  // armed rank split already done (see split_world)
+    // -u 0 dive: parent-window cap of iteration t (0: none). A solve that starts without
+    // an incumbent expands at most this many parents per iteration — the top of the
+    // stack, so the search dives depth-first to its first leaves (ref pfsp_c.c:55-63,
+    // DFS from +inf) — and the cap widens by 2^dive_shift per iteration once a leaf set
+    // the incumbent, back to the full window
+    unsigned cap;
+    unsigned cpad;  // the incumbent iteration t-1 saw (dive: widen when it stops improving)
   };
   Slot slot[3];
   // plain counters, updated by workgroup 0 (or the host between launches)
@@ -56,7 +63,7 @@ struct PoolCtl {
   // drop the replicated counts gathered so far. Same line as `bot`.
   int split_world;    // <= 1: no split armed
   int split_rank;
-  int pad0;
+  int dive_shift;     // -u 0 dive: log2 of the cap's growth per iteration after the first leaf
   u64 split_min;
   // nodes pushed and leaves counted inside subtrees a thread explored to the end (N-Queens
   // finishing: 64-bit counts, one accumulator line per 8th of the grid; the host folds them)
@@ -297,6 +304,7 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   v.S = ctl->slot[s_in].stack;
   v.nch_in = ctl->slot[s_in].nch;
   const int done_in = ctl->slot[s_in].sdone;
+  const unsigned cap_in = ctl->slot[s_in].cap;
   v.bot = ctl->bot;
   v.sworld = ctl->split_world;
   v.srank = ctl->split_rank;
@@ -317,6 +325,8 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
       ctl->slot[s_out].stack = 0;
       ctl->slot[s_out].nch = 0;
       ctl->slot[s_out].sdone = done_in;
+      ctl->slot[s_out].cap = cap_in;
+      ctl->slot[s_out].cpad = ctl->slot[s_in].cpad;
 #ifdef TTS_ILOG_BUILD  // (probe builds only: its live values made the front kernel spill)
       if (pa.ilog) ilog_record(pa.ilog, wall_clock64(), 0, 0, 0, 0, 0, 0, 0, 0, ctl->tree, t);
 #endif
@@ -326,6 +336,9 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
   // uniform by construction: readfirstlane keeps the window arithmetic in SGPRs
   v.C = static_cast<u64>(__builtin_amdgcn_readfirstlane(build_prefix(pa.cnt[b_in], v.nch_in, ps)));
   v.B = min(v.S + v.C, static_cast<u64>(pa.max_parents));
+  // the dive cap never applies while a rank split is pending (the split iteration needs
+  // the whole replicated pool in its window)
+  if (cap_in != 0 && !(v.sworld > 1 && !done_in)) v.B = min(v.B, static_cast<u64>(cap_in));
   const bool armed = v.sworld > 1 && !done_in && v.B > 0;
   v.armed = armed;
   // Local DFS when the pool holds a backlog of pa.local_min parents (default: four
@@ -421,6 +434,20 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
       ctl->slot[s_out].stack = v.overflow ? v.S : v.Snew;
       ctl->slot[s_out].nch = v.overflow ? 0 : v.nchunks + v.qn;
       ctl->slot[s_out].sdone = (done_in || v.split) ? 1 : 0;
+      {
+        // the dive cap holds until a leaf set the incumbent, then widens geometrically
+        // (dive_shift bit 8: hold the cap while the incumbent still improves, like a DFS
+        // that keeps finding better leaves; widen once an iteration brought no improvement)
+        unsigned cap = cap_in;
+        const unsigned b = static_cast<unsigned>(__hip_atomic_load(&ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const unsigned prev = ctl->slot[s_in].cpad;
+        if (cap != 0 && b != 0x7fffffffu && !((ctl->dive_shift & 0x100) && b < prev)) {
+          const u64 w = static_cast<u64>(cap) << max(0, min(ctl->dive_shift & 0xff, 16));
+          cap = w >= static_cast<u64>(pa.max_parents) ? 0u : static_cast<unsigned>(w);
+        }
+        ctl->slot[s_out].cap = cap;
+        ctl->slot[s_out].cpad = b;
+      }
       if (v.split && v.srank != 0) {
         // everything counted so far was explored identically by every rank: rank 0 keeps it
         ctl->tree = 0;

@@ -15,8 +15,11 @@
 
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -74,6 +77,8 @@ class RcclTransport final : public DeviceResource {
     hctl_ = nullptr;
     if (own_) (void)hipStreamDestroy(own_);
     own_ = nullptr;
+    if (ev_) (void)hipEventDestroy(ev_);
+    ev_ = nullptr;
     if (comm_) (void)ncclCommDestroy(comm_);
     comm_ = nullptr;
   }
@@ -129,7 +134,12 @@ class RcclTransport final : public DeviceResource {
   // — after the previous round's send / recv there, so two collectives of this
   // communicator are never in flight at once — and the host waits for the gathered
   // (world, n) block to land in pinned memory. No Python, no second communicator.
-  void allgather_i64(const int64_t* v, int n, int64_t* out, IEngine& e) {
+  //
+  // The wait is bounded by timeout_s (parallel/comm.py sets the job's): a dead or diverged
+  // peer aborts the communicator (ncclCommAbort) and the call throws, so the round loop
+  // fails instead of hanging every rank. `idle` runs while the collective is pending.
+  void allgather_i64(const int64_t* v, int n, int64_t* out, IEngine& e,
+                     const std::function<void()>& idle = std::function<void()>()) {
     if (released_) throw std::runtime_error("RCCL transport closed");
     if (n < 0 || n > kCtlVals) throw std::invalid_argument("RcclTransport::allgather_i64: at most 16 values");
     TTS_HIP_CHECK(hipSetDevice(device_));
@@ -140,7 +150,7 @@ class RcclTransport final : public DeviceResource {
       TTS_HIP_CHECK(hipHostMalloc(&hctl_, static_cast<size_t>(world_) * kCtlVals * sizeof(int64_t), hipHostMallocDefault));
     }
     if (n == 0) {
-      TTS_HIP_CHECK(hipStreamSynchronize(xs));
+      wait_bounded(xs, idle);
       return;
     }
     std::memcpy(hctl_ + static_cast<size_t>(rank_) * n, v, sizeof(int64_t) * n);
@@ -149,11 +159,13 @@ class RcclTransport final : public DeviceResource {
     TTS_NCCL_CHECK(ncclAllGather(dctl_ + static_cast<size_t>(rank_) * n, dctl_, static_cast<size_t>(n), ncclInt64,
                                  comm_, xs));
     TTS_HIP_CHECK(hipMemcpyAsync(hctl_, dctl_, sizeof(int64_t) * n * world_, hipMemcpyDeviceToHost, xs));
-    TTS_HIP_CHECK(hipStreamSynchronize(xs));
+    wait_bounded(xs, idle);
     std::memcpy(out, hctl_, sizeof(int64_t) * n * world_);
     ++collectives_;
   }
   unsigned long long collectives() const { return collectives_; }
+  double timeout_s() const { return timeout_s_; }
+  void set_timeout_s(double t) { timeout_s_ = t; }
 
   // World-1 check of the whole path on one GPU: n nodes go pool -> staging -> RCCL send
   // to self / receive from self -> staging -> pool. Returns the nodes moved.
@@ -242,6 +254,32 @@ class RcclTransport final : public DeviceResource {
   }
 
  private:
+  // Wait for everything queued on xs, at most timeout_s: on expiry the communicator is
+  // aborted (its pending operations end) and the call throws.
+  void wait_bounded(hipStream_t xs, const std::function<void()>& idle) {
+    if (!ev_) TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming));
+    TTS_HIP_CHECK(hipEventRecord(ev_, xs));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 0;; ++spins) {
+      const hipError_t q = hipEventQuery(ev_);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) TTS_HIP_CHECK(q);
+      if (idle) idle();
+      if ((spins & 255) == 255) {
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (timeout_s_ > 0 && dt > timeout_s_) {
+          if (comm_) (void)ncclCommAbort(comm_);
+          comm_ = nullptr;
+          released_ = true;
+          throw std::runtime_error("rank " + std::to_string(rank_) + ": RCCL round all-gather did not complete in " +
+                                   std::to_string(timeout_s_) + " s (a peer died or left the round loop); "
+                                   "communicator aborted");
+        }
+        std::this_thread::yield();
+      }
+    }
+  }
+
   // Staging block `which` (0 out, 1 in) of at least `bytes`; a grown block replaces the
   // old one only after the transfer stream has drained (an RCCL op may still read it).
   void* staging(int which, size_t bytes, hipStream_t xs) {
@@ -268,6 +306,8 @@ class RcclTransport final : public DeviceResource {
   int64_t* dctl_ = nullptr;   // (world, n) gathered status, device
   int64_t* hctl_ = nullptr;   // pinned host image
   hipStream_t own_ = nullptr;  // for engines without a transfer stream
+  hipEvent_t ev_ = nullptr;    // completion of a bounded wait
+  double timeout_s_ = 1800.0;
   unsigned long long collectives_ = 0;
   ncclComm_t comm_ = nullptr;
   bool released_ = false;
@@ -284,8 +324,8 @@ class RcclRoundControl final : public RoundControl {
   RcclRoundControl(RcclTransport* t, IEngine* e) : t_(t), e_(e) {}
   int rank() const override { return t_->rank(); }
   int world() const override { return t_->world(); }
-  void allgather(const int64_t* v, int n, int64_t* out, const std::function<void()>&) override {
-    t_->allgather_i64(v, n, out, *e_);
+  void allgather(const int64_t* v, int n, int64_t* out, const std::function<void()>& idle) override {
+    t_->allgather_i64(v, n, out, *e_, idle);
   }
 
  private:

@@ -58,6 +58,16 @@ class EngineOptions:
     # front_dyn): time budget of one iteration in us, work shared between the workgroups of
     # an XCD; 0 = fixed-step local iterations
     dyn_us: int = 0
+    # -u 0 dive (csrc/hip/pool_device.hpp Slot::cap): a device solve begun without an
+    # incumbent expands at most dive_window parents (the top of the stack) per iteration
+    # until its first leaf, then the cap grows 2^dive_shift-fold per iteration back to
+    # max_parents; every node is counted (reference -u 0 semantics: a search from +inf).
+    # TTS_DIVE_WINDOW / TTS_DIVE_SHIFT override; 0 = off. 4096 / 2 on one MI355X (trees from
+    # +inf, no dive -> dive): ta014 LB1 99-162 M -> 102 M nodes (9.3 -> 6.2 ms), ta008 LB1_d 273 ->
+    # 230 M, ta003 LB1 232 -> 196 M (profiles/r6/dive_probe.txt; narrower windows and the
+    # hold-while-improving growth were better on one instance and worse on another)
+    dive_window: int = 4096
+    dive_shift: int = 2
 
 
 def make_multi(model, backend: str, device: int, opts: EngineOptions):
@@ -118,15 +128,18 @@ class PfspModel:
         return self.best_known if ub == 1 else INT_MAX
 
     def search_best(self, ub: int = 1) -> int:
-        """Initial incumbent of a device / distributed search: -u 1 as initial_best; -u 0
-        the best complete schedule of two host heuristics (csrc/core/pfsp_bounds_cpu.hpp):
-        a beam dive of LB1 and NEH + iterated greedy (TTS_NEH_BUDGET cell updates, ~5 ms),
-        so the breadth-first device windows prune from the first iteration (ta014 -u 0
-        explored 632 M nodes from +inf, profiles/r4/live_best_u0.txt). TTS_DIVE=0 starts
-        from +inf as the reference does; TTS_DIVE=<beam> sets the beam width (default 32)."""
+        """Initial incumbent of a device / distributed search. -u 1: as initial_best. -u 0:
+        +inf, the reference's semantics (ref pfsp_c.c:55-63); the device engines then dive
+        depth-first to their first leaves through a narrow parent window
+        (EngineOptions.dive_window) and every node of that dive is counted.
+        Opt-in (TTS_DIVE=<beam>, CLI --heuristic-ub): start from the best complete schedule of
+        two host heuristics (csrc/core/pfsp_bounds_cpu.hpp) — a beam dive of LB1 and NEH +
+        iterated greedy (TTS_NEH_BUDGET cell updates, ~5 ms). That tree is then NOT the
+        reference's -u 0 quantity: the initial incumbent is recorded with the results
+        (initial_ub)."""
         if ub == 1:
             return self.best_known
-        beam = int(os.environ.get("TTS_DIVE", "32"))
+        beam = int(os.environ.get("TTS_DIVE", "0"))
         if beam <= 0:
             return INT_MAX
         if self._dive is None:
@@ -175,7 +188,9 @@ class PfspModel:
                                   max_parents=opts.max_parents, ring_bytes=opts.ring_bytes,
                                   iters_small=opts.iters_small, iters_large=opts.iters_large,
                                   use_graphs=opts.use_graphs, taillard_id=self.inst_id,
-                                  iters_first=opts.iters_first, dyn_us=opts.dyn_us)
+                                  iters_first=opts.iters_first, dyn_us=opts.dyn_us,
+                                  dive_window=int(os.environ.get("TTS_DIVE_WINDOW", opts.dive_window)),
+                                  dive_shift=int(os.environ.get("TTS_DIVE_SHIFT", opts.dive_shift)))
 
     def make_hybrid(self, engine, backend: str, threads: int, m: int = 25, cap: int = 20000, batch: int = 5000):
         """`engine` plus a CPU worker of `threads` threads as one rank engine

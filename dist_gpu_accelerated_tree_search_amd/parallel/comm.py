@@ -215,7 +215,9 @@ class Comm:
         t = torch.tensor(list(uid), dtype=torch.uint8, device=self.device)
         dist.broadcast(t, src=0)
         uid = bytes(t.cpu().tolist())
-        return H.RcclTransport(uid, self.rank, self.world, self.device.index)
+        tr = H.RcclTransport(uid, self.rank, self.world, self.device.index)
+        tr.timeout_s = float(self.timeout_s)  # bounded round all-gathers (dead peer -> abort + raise)
+        return tr
 
     def transport(self, engine, node_bytes: int):
         """What the native round loop moves nodes with: the native RCCL transport for a

@@ -21,6 +21,10 @@ def build_model(spec: dict):
 def solve_rank(spec: dict) -> dict:
     """Solve spec's problem cooperatively on all ranks of the current process group."""
     backend = spec.get("backend", "gpu")
+    if spec.get("heuristic_ub"):  # CLI --heuristic-ub: -u 0 from the host heuristics' incumbent
+        import os
+
+        os.environ.setdefault("TTS_DIVE", "32")
     # comm on the GPU (RCCL) unless asked for gloo, e.g. several ranks sharing one GPU
     if backend == "gpu" and "device" in spec and spec.get("comm", "nccl") == "nccl":
         raise ValueError("spec['device'] puts ranks on one GPU: RCCL needs one GPU per rank, use comm='gloo'")

@@ -19,7 +19,9 @@ BANNER = "================================================="
 
 
 def pfsp_settings(inst: int, machines: int, jobs: int, ub: int, lb: int, D: int, C: int, ws: int, comm_size: int,
-                  L: int, version: int) -> str:
+                  L: int, version: int, init_ub: int | None = None) -> str:
+    """init_ub: with -u 0, the opt-in heuristic starting incumbent (--heuristic-ub), printed
+    instead of "inf" so the explored tree is not mistaken for the reference's -u 0 tree."""
     if version == 0:
         head = "Sequential C++"
     elif version == 1:
@@ -35,7 +37,9 @@ def pfsp_settings(inst: int, machines: int, jobs: int, ub: int, lb: int, D: int,
         head,
         "",
         f"Resolution of PFSP Taillard's instance: ta{inst} (m = {machines}, n = {jobs})",
-        "Initial upper bound: inf" if ub == 0 else "Initial upper bound: opt",
+        ("Initial upper bound: opt" if ub != 0 else
+         "Initial upper bound: inf" if init_ub is None or init_ub >= 2**31 - 1 else
+         f"Initial upper bound: heuristic ({init_ub})"),
         f"Lower bound function: {LB_NAMES.get(lb, 'lb2')}",
         "Branching rule: fwd",
         BANNER,

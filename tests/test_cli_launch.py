@@ -67,3 +67,33 @@ def test_rank_spec_device_needs_gloo():
 
     with pytest.raises(ValueError, match="gloo"):
         solve_rank({"problem": "pfsp", "backend": "gpu", "device": 0, "comm": "nccl"})
+
+
+def test_heuristic_ub_is_opt_in_and_recorded(tmp_path, monkeypatch, capsys):
+    # -u 0 prints "inf" (the reference's semantics) unless --heuristic-ub asks for the host
+    # heuristics' incumbent, which is then printed and recorded (CPU run: -D 0 ignores it)
+    import json
+
+    from dist_gpu_accelerated_tree_search_amd.models.pfsp import PfspModel
+    from dist_gpu_accelerated_tree_search_amd.utils import report
+
+    monkeypatch.delenv("TTS_DIVE", raising=False)
+    assert "Initial upper bound: inf" in report.pfsp_settings(14, 10, 20, 0, 1, 1, 0, 1, 1, 1, 2, None)
+    assert "heuristic (1400)" in report.pfsp_settings(14, 10, 20, 0, 1, 1, 0, 1, 1, 1, 2, 1400)
+
+    class A:
+        ub, D, heuristic_ub = 0, 1, False
+
+    m = PfspModel(14, 1)
+    assert cli._init_ub(A, m) is None
+    A.heuristic_ub = True
+    monkeypatch.setenv("TTS_DIVE", "32")
+    assert 1377 <= cli._init_ub(A, m) < 1500
+    A.ub = 1
+    assert cli._init_ub(A, m) == 1377
+    out = tmp_path / "r.json"
+    monkeypatch.delenv("TTS_DIVE", raising=False)
+    assert cli.main(["pfsp", "-i", "2", "-l", "1", "-u", "0", "-D", "0", "--no-csv", "--json", str(out)]) == 0
+    assert "Initial upper bound: inf" in capsys.readouterr().out
+    rec = json.loads(out.read_text().splitlines()[-1])
+    assert rec["initial_ub"] is None and rec["best"] == 1359

@@ -74,8 +74,8 @@ def test_queens_14_sequential():
 
 
 @pytest.mark.parametrize("inst,beam", [(14, 32), (21, 32), (1, 8), (31, 8)])
-def test_beam_dive_gives_a_real_schedule_makespan(inst, beam):
-    # -u 0 device searches start from the dive's makespan: a complete schedule's, so
+def test_beam_dive_gives_a_real_schedule_makespan(inst, beam, monkeypatch):
+    # opt-in (TTS_DIVE): -u 0 device searches start from the dive's makespan: a complete schedule's, so
     # never below the optimum (Taillard's best known for these solved instances), and
     # close to it (within 10 %)
     import itertools  # noqa: F401
@@ -88,7 +88,17 @@ def test_beam_dive_gives_a_real_schedule_makespan(inst, beam):
     assert m.best_known <= v <= 1.25 * m.best_known, (v, m.best_known)
     h = ops.cpu().pfsp_neh(m.native, 2_000_000)  # NEH + iterated greedy: within 3 %
     assert m.best_known <= h <= 1.03 * m.best_known, (h, m.best_known)
+    monkeypatch.setenv("TTS_DIVE", str(beam))
     assert m.search_best(0) == min(v, ops.cpu().pfsp_neh(m.native, 5_000_000))
+
+
+def test_u0_starts_from_inf_by_default(monkeypatch):
+    # the reference's -u 0 semantics: no heuristic incumbent unless asked for
+    from dist_gpu_accelerated_tree_search_amd.models.pfsp import INT_MAX, PfspModel
+
+    monkeypatch.delenv("TTS_DIVE", raising=False)
+    assert PfspModel(14, 1).search_best(0) == INT_MAX
+    assert PfspModel(14, 1).search_best(1) == 1377
 
 
 def test_beam_dive_exact_on_tiny_instances():

@@ -1,0 +1,41 @@
+"""-u 0 device dive (csrc/hip/pool_device.hpp Slot::cap): a solve begun without an
+incumbent expands a narrow window from the top of the stack until its first leaf, then
+widens. Every node is counted, so the result is a search from +inf (ref pfsp_c.c:55-63)."""
+import pytest
+
+from dist_gpu_accelerated_tree_search_amd.models.pfsp import INT_MAX, EngineOptions, PfspModel
+from dist_gpu_accelerated_tree_search_amd.search import solve_cpu, solve_engine
+
+pytestmark = pytest.mark.gpu
+
+GOLD14 = (2573652, 2648, 1377)
+
+
+@pytest.mark.parametrize("window,shift", [(0, 2), (1, 1), (64, 2), (1024, 2), (4096, 3)])
+def test_dive_finds_optimum_from_inf(window, shift, monkeypatch):
+    monkeypatch.delenv("TTS_DIVE", raising=False)
+    m = PfspModel(14, 1)
+    eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=1 << 30, dive_window=window, dive_shift=shift))
+    r = solve_engine(m, eng, ub=0)
+    assert r.best == 1377 and r.tree >= GOLD14[0]
+    # the cap only acts without an incumbent: the -u 1 tree is unchanged, also after a dive
+    r = solve_engine(m, eng, ub=1)
+    assert (r.tree, r.sol, r.best) == GOLD14
+
+
+@pytest.mark.parametrize("seed,lb", [(3, 0), (4, 1), (5, 2)])
+def test_dive_small_instances_match_host_optimum(seed, lb, monkeypatch):
+    monkeypatch.delenv("TTS_DIVE", raising=False)
+    m = PfspModel.synthetic(11, 5, seed, lb=lb)
+    want = solve_cpu(m, ub=0).best
+    eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=1 << 28, max_parents=1 << 16, dive_window=16))
+    r = solve_engine(m, eng, ub=0, best=INT_MAX)
+    assert r.best == want
+
+
+def test_dive_ta008_lb1d(monkeypatch):
+    monkeypatch.delenv("TTS_DIVE", raising=False)
+    m = PfspModel(8, 0)
+    eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=4 << 30))
+    r = solve_engine(m, eng, ub=0)
+    assert r.best == 1206 and r.tree >= 113458723
