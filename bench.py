@@ -98,7 +98,7 @@ def main() -> int:
     ap.add_argument("--no-extras", action="store_true", help="headline only (no ta021 / ta056 runs)")
     ap.add_argument("--extras", default="ta021,ta056,nq17", help="comma list of extras to run")
     ap.add_argument("--box-s", type=float, default=10.0, help="ta056 LB2 time box (seconds)")
-    ap.add_argument("--extras-timeout", type=float, default=900.0,
+    ap.add_argument("--extras-timeout", type=float, default=300.0,
                     help="watchdog: print the line and end every rank after this many seconds of extras")
     ap.add_argument("--extra-inst-lb1d", type=int, default=21, help=argparse.SUPPRESS)
     ap.add_argument("--extra-inst-lb2", type=int, default=56, help=argparse.SUPPRESS)
@@ -237,6 +237,29 @@ def main() -> int:
     return 0
 
 
+def _make_solver(model, a, device: int, opts, comm, cfg):
+    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistSolver
+
+    engine = model.make_engine(a.backend, device, opts)
+    return engine, DistSolver(model, engine, comm, cfg, window=opts.max_parents)
+
+
+def _agreed_setup(comm, name: str, build):
+    """Engine + solver of an extra on every rank, then one agreement: if any rank failed
+    to set up (e.g. device memory), every rank raises before the collective solve, so no
+    rank waits in a solve that another rank never enters."""
+    made, err = None, None
+    try:
+        made = build()
+    except Exception as e:  # noqa: BLE001 - agreed on below, re-raised on every rank
+        err = e
+        log(f"rank {comm.rank}: extra {name} setup failed: {e!r}")
+    if not bool(comm.allreduce_i64([0 if err else 1], "min")[0]):
+        made = None
+        raise RuntimeError(f"{name}: setup failed on some rank" + (f" (here: {err!r})" if err else ""))
+    return made
+
+
 QUEENS_GOLDEN = {17: (8017021931, 95815104), 16: (1141190302, 14772512), 12: (856188, 14200), 11: (166925, 2680)}
 QUEENS_REF_S = {17: 807.0}  # reference nqueens_c.out -N 17, sequential (BASELINE.md)
 
@@ -245,7 +268,7 @@ def run_queens_extra(a, comm, device: int, N: int) -> dict:
     """N-Queens N (g=1): best of 3 cooperative solves with the headline's runtime."""
     from dist_gpu_accelerated_tree_search_amd.models.nqueens import QueensModel
     from dist_gpu_accelerated_tree_search_amd.models.pfsp import EngineOptions
-    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig, DistSolver
+    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig
 
     model = QueensModel(N, 1)
     # two engines per GPU with the solve split between them in the graph: N=17 74 -> 48 ms
@@ -253,9 +276,8 @@ def run_queens_extra(a, comm, device: int, N: int) -> dict:
     opts = EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30, streams=2, stream_split=512) \
         if a.backend == "gpu" else EngineOptions(streams=2, stream_split=8)
     t_setup = time.perf_counter()
-    engine = model.make_engine(a.backend, device, opts)
-    solver = DistSolver(model, engine, comm, DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws),
-                        window=opts.max_parents)
+    engine, solver = _agreed_setup(comm, f"N-Queens N={N}", lambda: _make_solver(
+        model, a, device, opts, comm, DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws)))
     t_setup = time.perf_counter() - t_setup
     best_dt, r = None, None
     for _ in range(3):
@@ -283,16 +305,15 @@ def run_solve_extra(a, comm, device: int, inst: int, lb: int, time_limit: float)
     """One cooperative solve (or a time box) of another BASELINE config on all ranks,
     with the headline's runtime (DistSolver: same Step 1, split and rounds)."""
     from dist_gpu_accelerated_tree_search_amd.models.pfsp import EngineOptions, PfspModel
-    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig, DistSolver
+    from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig
 
     model = PfspModel(inst, lb)
     # big trees: several engines per GPU fill it better than one (profiles/r3/streams*.txt)
     opts = EngineOptions(ring_bytes=int(a.extra_ring_gb * (1 << 30)), streams=max(1, a.extra_streams),
                          max_parents=a.extra_max_parents)
     t_setup = time.perf_counter()
-    engine = model.make_engine(a.backend, device, opts)
     cfg = DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws, time_limit_s=time_limit)
-    solver = DistSolver(model, engine, comm, cfg, window=opts.max_parents)
+    engine, solver = _agreed_setup(comm, f"ta{inst:03d}", lambda: _make_solver(model, a, device, opts, comm, cfg))
     t_setup = time.perf_counter() - t_setup
     comm.barrier()
     t0 = time.perf_counter()

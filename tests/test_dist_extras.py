@@ -235,3 +235,36 @@ def test_multi_engine_in_session():
     res = spawn_local(2, solve_rank, (spec,), timeout=300)
     for r in res:
         assert (r["tree"], r["sol"], r["best"]) == GOLD
+
+
+def _agreed_setup_rank(fail_rank: int) -> str:
+    import importlib.util
+
+    from dist_gpu_accelerated_tree_search_amd.parallel.comm import Comm
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    comm = Comm(use_gpu=False)
+    try:
+        def build():
+            if comm.rank == fail_rank:
+                raise MemoryError("no device memory (injected)")
+            return "engine", "solver"
+
+        try:
+            bench._agreed_setup(comm, "ta021", build)
+            return "ok"
+        except RuntimeError as e:
+            return str(e)
+    finally:
+        comm.close()
+
+
+def test_extra_setup_failure_on_one_rank_stops_every_rank():
+    # an extra whose engine cannot be built on one rank (device memory) must not leave the
+    # other ranks waiting in a collective solve: every rank learns it and raises
+    res = spawn_local(3, _agreed_setup_rank, (1,), timeout=120)
+    assert all("setup failed on some rank" in r for r in res), res
+    assert "injected" in res[1] and "injected" not in res[0]
+    assert spawn_local(2, _agreed_setup_rank, (-1,), timeout=120) == ["ok", "ok"]
