@@ -27,6 +27,7 @@ def main() -> int:
     ap.add_argument("--worlds", default="")
     ap.add_argument("--world-window", type=int, default=1024)
     ap.add_argument("--world-shift", type=int, default=2)
+    ap.add_argument("--max-parents", type=int, default=1 << 18)
     a = ap.parse_args()
     warm_forkserver()
     from dist_gpu_accelerated_tree_search_amd.models.pfsp import EngineOptions, PfspModel
@@ -45,7 +46,7 @@ def main() -> int:
             heur = w == "heur"
             os.environ["TTS_DIVE"] = "32" if heur else "0"
             eng = model.make_engine("gpu", 0, EngineOptions(ring_bytes=8 << 30, dive_window=0 if heur else w,
-                                                            dive_shift=s))
+                                                            dive_shift=s, max_parents=a.max_parents))
             ts, r, trees = [], None, []
             for _ in range(a.repeat):
                 t0 = time.perf_counter()
@@ -60,7 +61,8 @@ def main() -> int:
         for world in (int(x) for x in a.worlds.split(",") if x):
             spec = {"problem": "pfsp", "inst": inst, "lb": lb, "backend": "gpu", "comm": "gloo", "device": 0,
                     "session": True, "ub": 0, "repeat": 1,
-                    "engine": {"ring_bytes": 4 << 30, "dive_window": a.world_window, "dive_shift": a.world_shift}}
+                    "engine": {"ring_bytes": 4 << 30, "dive_window": a.world_window, "dive_shift": a.world_shift,
+                               "max_parents": a.max_parents}}
             trees, ts = [], []
             for _ in range(a.repeat):
                 res = spawn_local(world, solve_rank, (spec,), timeout=600, env={"TTS_DIVE": "0"})
