@@ -15,6 +15,7 @@ import torch  # noqa: F401,E402
 from dist_gpu_accelerated_tree_search_amd import EngineOptions, PfspModel  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+per_rank = int(sys.argv[2]) if len(sys.argv) > 2 else 512  # split_min = per_rank * world (DistConfig.split_per_rank)
 m = PfspModel(14, 1)
 eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 19, ring_bytes=32 << 30))
 for world in (1, 2, 4, 8):
@@ -22,7 +23,7 @@ for world in (1, 2, 4, 8):
     for rep in range(reps + 5):
         nodes, t1, s1, best = m.warmup(m.initial_best(1), 25)
         if world > 1:
-            eng.set_split(0, world, 512 * world)
+            eng.set_split(0, world, per_rank * world)
         t0 = time.perf_counter()
         eng.begin(nodes, int(best))
         eng.run()
