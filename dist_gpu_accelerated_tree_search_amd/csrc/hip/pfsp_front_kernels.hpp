@@ -290,12 +290,42 @@ __device__ inline void front_broadcast(const PfspFrontArgs<M, NJ>& a, const uint
 template <int M, int NJ>
 __device__ inline void front_remain(const FrontSmem<M, NJ>& sm, const uint32_t (&w)[FrontGeom<M, NJ>::NW],
                                     uint32_t (&r2)[FrontGeom<M, NJ>::HW]) {
+  constexpr int HW = FrontGeom<M, NJ>::HW;
 #pragma unroll
-  for (int h = 0; h < FrontGeom<M, NJ>::HW; ++h) r2[h] = 0;
-  for (auto x = front_mask<M, NJ>(w); x; x &= x - 1) {
-    const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[mask_ctz(x)]);
+  for (int h = 0; h < HW; ++h) r2[h] = 0;
+  if constexpr (M <= 10) {
+    // 4 jobs per pass, every row read issued before the first add: one LDS latency per
+    // pass instead of one per job (the rolled loop waited on each row in turn; ta014
+    // headline -0.9 % same box, profiles/r6/remain_ab.txt). 20 machines keep the rolled
+    // loop (its registers are the kernel's budget).
+    constexpr int U = 4;
+    for (auto x = front_mask<M, NJ>(w); x;) {
+      int j[U];
+      bool ok[U];
 #pragma unroll
-    for (int h = 0; h < FrontGeom<M, NJ>::HW; ++h) r2[h] += row[h];
+      for (int u = 0; u < U; ++u) {
+        ok[u] = x != 0;
+        j[u] = ok[u] ? mask_ctz(x) : 0;
+        x &= x - 1;
+      }
+      uint32_t rw[U][HW];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[j[u]]);
+#pragma unroll
+        for (int h = 0; h < HW; ++h) rw[u][h] = row[h];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int h = 0; h < HW; ++h) r2[h] += ok[u] ? rw[u][h] : 0u;
+    }
+  } else {
+    for (auto x = front_mask<M, NJ>(w); x; x &= x - 1) {
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(sm.ptab[mask_ctz(x)]);
+#pragma unroll
+      for (int h = 0; h < HW; ++h) r2[h] += row[h];
+    }
   }
 }
 
