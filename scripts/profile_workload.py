@@ -147,6 +147,11 @@ elif which.startswith("spill014"):  # spill014[:ring_MB]: ta014 LB1 solved to th
         raise SystemExit(0)
     del eng
     raise SystemExit(0)
+elif which == "queens17":  # the bench's N-Queens extra: N=17, two split engines on the GPU
+    m = QueensModel(17)
+    eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30, streams=2, stream_split=512))
+    for _ in range(2):
+        r = solve_engine(m, eng)
 elif which == "queens":
     m = QueensModel(16); eng = m.make_engine("gpu", 0, EngineOptions(max_parents=1 << 20, ring_bytes=32 << 30))
     r = solve_engine(m, eng)
