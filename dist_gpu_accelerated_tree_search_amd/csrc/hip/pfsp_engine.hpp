@@ -461,6 +461,96 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
   }
 }
 
+// Element-wise probe of the permutation-node LB1 / LB1_d expand kernel (instances of
+// more than 50 jobs; 20 / 50 jobs under TTS_FRONT=0): ONE iteration over `n` parents
+// loaded as the window. Returns every child's bound (parent order, children
+// k = depth..N-1), the children the kernel wrote (chunk order; lb < best, the leaves of
+// depth N-1 parents excluded), the leaves it counted and the incumbent after the launch.
+struct Lb1ProbeResult {
+  std::vector<int> bounds;
+  std::vector<uint8_t> children;
+  long long leaves = 0;
+  int best = 0;
+};
+
+template <int NJ, int M>
+Lb1ProbeResult pfsp_lb1_expand_probe_t(const PfspInstance& in, const void* parents, size_t n, int best, int device) {
+  using Node = PfspNode<NJ>;
+  using G = dev::PfspGeom<NJ, 1, M>;
+  TTS_HIP_CHECK(hipSetDevice(device));
+  const Node* ph = static_cast<const Node*>(parents);
+  Lb1ProbeResult res;
+  std::vector<int> offsets(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    if (ph[i].depth >= in.jobs) throw std::invalid_argument("lb1 expand probe: parents must have children");
+    offsets[i + 1] = offsets[i] + (in.jobs - ph[i].depth);
+  }
+  res.bounds.assign(static_cast<size_t>(offsets[n]), -1);
+  res.best = best;
+  if (n == 0) return res;
+  const size_t nchunks = (n + G::BP - 1) / G::BP;
+  if (nchunks > static_cast<size_t>(G::MAXCHUNKS)) throw std::invalid_argument("lb1 expand probe: too many parents");
+  dev::PfspArgs<NJ, M> a{};
+  const PfspTableImages img = pfsp_fill_args(in, a);
+  std::vector<void*> owned;
+  auto up = [&](const auto& v) {
+    auto* d = upload_vec(v);
+    owned.push_back(const_cast<void*>(static_cast<const void*>(d)));
+    return d;
+  };
+  auto dalloc = [&](size_t bytes) {
+    void* d = nullptr;
+    TTS_HIP_CHECK(hipMalloc(&d, std::max<size_t>(bytes, 16)));
+    TTS_HIP_CHECK(hipMemset(d, 0, std::max<size_t>(bytes, 16)));
+    owned.push_back(d);
+    return d;
+  };
+  a.ptab = up(img.ptab);
+  a.dbg_off = up(offsets);
+  a.dbg_lb = up(res.bounds);
+  size_t cap = 1;
+  while (cap < n) cap *= 2;
+  auto& pa = a.pool;
+  pa.ring = static_cast<Node*>(dalloc(cap * sizeof(Node)));
+  TTS_HIP_CHECK(hipMemcpy(pa.ring, ph, n * sizeof(Node), hipMemcpyHostToDevice));
+  for (int b = 0; b < 2; ++b) {
+    pa.buf[b] = static_cast<Node*>(dalloc(nchunks * G::SLOT * sizeof(Node)));
+    pa.cnt[b] = static_cast<int*>(dalloc(nchunks * sizeof(int)));
+    pa.lcnt[b] = static_cast<int*>(dalloc(nchunks * sizeof(int)));
+  }
+  dev::PoolCtl h{};
+  h.slot[0].stack = n;
+  h.best.v = best;
+  pa.ctl = static_cast<dev::PoolCtl*>(dalloc(sizeof(dev::PoolCtl)));
+  TTS_HIP_CHECK(hipMemcpy(pa.ctl, &h, sizeof(h), hipMemcpyHostToDevice));
+  pa.mirror = nullptr;
+  pa.cap_mask = cap - 1;
+  pa.max_parents = static_cast<int>(nchunks * G::BP);
+  pa.max_chunks = static_cast<int>(nchunks);
+  hipLaunchKernelGGL((dev::pfsp_expand_kernel<NJ, M, 1>), dim3(static_cast<unsigned>(std::min<size_t>(nchunks, 1024))),
+                     dim3(dev::kBlock), 0, 0, a, 0);
+  TTS_HIP_CHECK(hipGetLastError());
+  TTS_HIP_CHECK(hipDeviceSynchronize());
+  TTS_HIP_CHECK(hipMemcpy(res.bounds.data(), a.dbg_lb, res.bounds.size() * sizeof(int), hipMemcpyDeviceToHost));
+  std::vector<int> cnt(nchunks), lcnt(nchunks);
+  TTS_HIP_CHECK(hipMemcpy(cnt.data(), pa.cnt[1], nchunks * sizeof(int), hipMemcpyDeviceToHost));
+  TTS_HIP_CHECK(hipMemcpy(lcnt.data(), pa.lcnt[1], nchunks * sizeof(int), hipMemcpyDeviceToHost));
+  for (size_t c = 0; c < nchunks; ++c) {
+    if (cnt[c] < 0 || static_cast<size_t>(cnt[c]) > static_cast<size_t>(G::SLOT))
+      throw std::runtime_error("lb1 expand probe: chunk count out of range");
+    const size_t at = res.children.size();
+    res.children.resize(at + static_cast<size_t>(cnt[c]) * sizeof(Node));
+    if (cnt[c])
+      TTS_HIP_CHECK(hipMemcpy(res.children.data() + at, pa.buf[1] + c * G::SLOT, static_cast<size_t>(cnt[c]) * sizeof(Node),
+                              hipMemcpyDeviceToHost));
+    res.leaves += lcnt[c] & 0xffff;
+  }
+  TTS_HIP_CHECK(hipMemcpy(&h, pa.ctl, sizeof(h), hipMemcpyDeviceToHost));
+  res.best = h.best.v;
+  for (void* d : owned) (void)hipFree(d);
+  return res;
+}
+
 template <int M, int NJ = 20>
 std::unique_ptr<IEngine> make_pfsp_front_engine_t(const PfspInstance& in, const EngineConfig& cfg) {
   TTS_HIP_CHECK(hipSetDevice(cfg.device));
@@ -740,6 +830,7 @@ std::vector<double> pfsp_front_time(const PfspInstance& in, int lb, const void* 
                                     const EngineConfig& cfg, int reps);
 // front-layout instances only (pfsp_front_ok), defined with the 20-job bucket (the
 // 50-job front bucket's in its own TU)
+Lb1ProbeResult pfsp_lb1_expand_probe(const PfspInstance& in, const void* parents, size_t n, int best, int device);
 FrontProbeResult pfsp_front_probe(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
                                   const EngineConfig& cfg, unsigned cap, int split_rank = 0, int split_world = 1,
                                   size_t split_min = 0);
@@ -754,7 +845,8 @@ std::vector<double> pfsp_front_time_nj50(const PfspInstance& in, int lb, const v
   std::vector<int> pfsp_gpu_bounds_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
                                           int device);                                                \
   std::vector<int> pfsp_expand_probe_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
-                                            int device, int variant, int reps, std::vector<double>* timing);
+                                            int device, int variant, int reps, std::vector<double>* timing); \
+  Lb1ProbeResult pfsp_lb1_expand_probe_nj##NJ(const PfspInstance& in, const void* parents, size_t n, int best, int device);
 TTS_PFSP_DECLARE_BUCKET(20)
 TTS_PFSP_DECLARE_BUCKET(50)
 TTS_PFSP_DECLARE_BUCKET(100)
@@ -791,6 +883,13 @@ TTS_PFSP_DECLARE_BUCKET(500)
     return with_machine_bucket(in.machines, [&](auto mm) {                                           \
       constexpr int M = decltype(mm)::value;                                                         \
       return pfsp_expand_probe_t<NJ, M, 2>(in, parents, n, best, device, variant, reps, timing);    \
+    });                                                                                              \
+  }                                                                                                  \
+  Lb1ProbeResult pfsp_lb1_expand_probe_nj##NJ(const PfspInstance& in, const void* parents, size_t n, int best, \
+                                              int device) {                                          \
+    return with_machine_bucket(in.machines, [&](auto mm) {                                           \
+      constexpr int M = decltype(mm)::value;                                                         \
+      return pfsp_lb1_expand_probe_t<NJ, M>(in, parents, n, best, device);                           \
     });                                                                                              \
   }
 

@@ -34,4 +34,14 @@ std::vector<int> pfsp_expand_probe(const PfspInstance& in, int lb, const void* p
   }
 }
 
+Lb1ProbeResult pfsp_lb1_expand_probe(const PfspInstance& in, const void* parents, size_t n, int best, int device) {
+  switch (pfsp_bucket(in.jobs)) {
+    case 20: return pfsp_lb1_expand_probe_nj20(in, parents, n, best, device);
+    case 50: return pfsp_lb1_expand_probe_nj50(in, parents, n, best, device);
+    case 100: return pfsp_lb1_expand_probe_nj100(in, parents, n, best, device);
+    case 200: return pfsp_lb1_expand_probe_nj200(in, parents, n, best, device);
+    default: return pfsp_lb1_expand_probe_nj500(in, parents, n, best, device);
+  }
+}
+
 }  // namespace tts

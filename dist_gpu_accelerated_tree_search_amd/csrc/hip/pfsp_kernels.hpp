@@ -93,8 +93,9 @@ struct PfspArgs {
   uint8_t pm1[PfspConsts<M>::P];
   // LB2 expand knob (after the tables so the LB1 kernels' argument layout is unchanged)
   int lb2_rounds;          // B2 in rounds of pairs, re-compacting the children still below best
-  // element-wise probe of the expand kernel (tests): bound of every child of window
-  // parent i at dbg_lb[dbg_off[i] + (k - depth)] (exact LB2 below best, else >= best)
+  // element-wise probe of the expand kernels (tests): bound of every child of window
+  // parent i at dbg_lb[dbg_off[i] + (k - depth)] (LB2: exact below best, else >= best;
+  // LB1 / LB1_d: exact)
   int* dbg_lb;
   const int* dbg_off;
   // LB2 records again, padded per pair to rs4 16-B vectors (two records each, zero
@@ -1085,6 +1086,7 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
     if (tid < nvalid) {
       const bool leaf = sm.node[tid].depth + 1 == a.jobs;
       pfsp_lb1_parent<NJ, M>(a, sm, tid, [&](int j, int k, int lb) {
+        if (a.dbg_lb) a.dbg_lb[a.dbg_off[first + tid] + j] = lb;  // element-wise probe (tests)
         const bool keep = split_keep(v, first + tid, k);
         if (leaf) {
           nleaf += keep;
