@@ -260,7 +260,34 @@ PYBIND11_MODULE(_tts_hip, m) {
       py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("lb"), py::arg("parents"), py::arg("best") = INT_MAX,
       py::arg("device") = 0, py::arg("variant") = 0,
       "One production expand iteration over these parents with the debug output on: every child's bound "
-      "(exact LB2 below best, else >= best). variant 0 prefix/suffix, 1 rounds, 2 dense, 3 wave.");
+      "(exact LB2 below best, else >= best). variant 1 rounds, 2 dense, 4 rounds of packed two-child walks.");
+  m.def(
+      "pfsp_expand_probe_out",
+      [](int jobs, int machines, std::vector<int> p, U8 parents, int best, int device, int variant) {
+        const PfspInstance in = make_instance(jobs, machines, std::move(p));
+        const size_t nb = with_pfsp_bucket(jobs, [](auto nj) { return sizeof(PfspNode<decltype(nj)::value>); });
+        if (parents.ndim() != 2 || static_cast<size_t>(parents.shape(1)) != nb)
+          throw std::invalid_argument("parents must be a (n, node_bytes) uint8 array");
+        ExpandProbeResult r;
+        {
+          py::gil_scoped_release nogil;
+          r.bounds = pfsp_expand_probe(in, 2, parents.data(), static_cast<size_t>(parents.shape(0)), best, device, variant,
+                                       0, nullptr, &r);
+        }
+        py::array_t<int> b(static_cast<py::ssize_t>(r.bounds.size()));
+        std::memcpy(b.mutable_data(), r.bounds.data(), r.bounds.size() * sizeof(int));
+        py::array_t<uint8_t> c({static_cast<py::ssize_t>(r.children.size() / nb), static_cast<py::ssize_t>(nb)});
+        if (!r.children.empty()) std::memcpy(c.mutable_data(), r.children.data(), r.children.size());
+        py::dict d;
+        d["bounds"] = b;
+        d["children"] = c;
+        d["leaves"] = r.leaves;
+        d["best"] = r.best;
+        return d;
+      },
+      py::arg("jobs"), py::arg("machines"), py::arg("p"), py::arg("parents"), py::arg("best") = INT_MAX,
+      py::arg("device") = 0, py::arg("variant") = 4,
+      "pfsp_expand_probe (LB2) plus what the iteration wrote: children (lb < best), leaves, incumbent.");
   m.def(
       "pfsp_lb1_expand_probe",
       [](int jobs, int machines, std::vector<int> p, U8 parents, int best, int device) {
@@ -268,7 +295,7 @@ PYBIND11_MODULE(_tts_hip, m) {
         const size_t nb = with_pfsp_bucket(jobs, [](auto nj) { return sizeof(PfspNode<decltype(nj)::value>); });
         if (parents.ndim() != 2 || static_cast<size_t>(parents.shape(1)) != nb)
           throw std::invalid_argument("parents must be a (n, node_bytes) uint8 array");
-        Lb1ProbeResult r;
+        ExpandProbeResult r;
         {
           py::gil_scoped_release nogil;
           r = pfsp_lb1_expand_probe(in, parents.data(), static_cast<size_t>(parents.shape(0)), best, device);

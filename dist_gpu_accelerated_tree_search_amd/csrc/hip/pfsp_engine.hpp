@@ -318,6 +318,15 @@ std::vector<int> pfsp_gpu_bounds_t(const PfspInstance& in, const void* parents, 
   return out;
 }
 
+// Output of the expand probes beyond the bounds: the children an iteration wrote (chunk
+// order), the leaves it counted and the incumbent after it.
+struct ExpandProbeResult {
+  std::vector<int> bounds;
+  std::vector<uint8_t> children;
+  long long leaves = 0;
+  int best = 0;
+};
+
 // Element-wise probe of the production expand kernel (LB2 only): ONE iteration
 // over `n` parents loaded as the window, with the kernel's debug output on. Returns
 // every child's bound in parent order (children k = depth..N-1): the exact LB2 when
@@ -330,7 +339,8 @@ std::vector<int> pfsp_gpu_bounds_t(const PfspInstance& in, const void* parents, 
 // phase A, B1, B2, B3+C shader clocks per chunk, chunks}.
 template <int NJ, int M, int LBK>
 std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents, size_t n, int best, int device,
-                                     int variant, int reps = 0, std::vector<double>* timing = nullptr) {
+                                     int variant, int reps = 0, std::vector<double>* timing = nullptr,
+                                     ExpandProbeResult* extra = nullptr) {
   using Node = PfspNode<NJ>;
   using G = dev::PfspGeom<NJ, LBK, M>;
   if constexpr (LBK != 2) {
@@ -398,6 +408,26 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
     launch(dim3(static_cast<unsigned>(std::min<size_t>(nchunks, 1024))));
     TTS_HIP_CHECK(hipDeviceSynchronize());
     TTS_HIP_CHECK(hipMemcpy(out.data(), a.dbg_lb, nb * sizeof(int), hipMemcpyDeviceToHost));
+    if (extra) {  // what the iteration wrote: per-chunk children (buffer 1), leaves, incumbent
+      std::vector<int> cnt(nchunks), lcnt(nchunks);
+      TTS_HIP_CHECK(hipMemcpy(cnt.data(), pa.cnt[1], nchunks * sizeof(int), hipMemcpyDeviceToHost));
+      TTS_HIP_CHECK(hipMemcpy(lcnt.data(), pa.lcnt[1], nchunks * sizeof(int), hipMemcpyDeviceToHost));
+      extra->children.clear();
+      extra->leaves = 0;
+      for (size_t c = 0; c < nchunks; ++c) {
+        if (cnt[c] < 0 || static_cast<size_t>(cnt[c]) > static_cast<size_t>(G::SLOT))
+          throw std::runtime_error("expand probe: chunk count out of range");
+        const size_t at = extra->children.size();
+        extra->children.resize(at + static_cast<size_t>(cnt[c]) * sizeof(Node));
+        if (cnt[c])
+          TTS_HIP_CHECK(hipMemcpy(extra->children.data() + at, pa.buf[1] + c * G::SLOT,
+                                  static_cast<size_t>(cnt[c]) * sizeof(Node), hipMemcpyDeviceToHost));
+        extra->leaves += lcnt[c] & 0xffff;
+      }
+      dev::PoolCtl hc{};
+      TTS_HIP_CHECK(hipMemcpy(&hc, pa.ctl, sizeof(hc), hipMemcpyDeviceToHost));
+      extra->best = hc.best.v;
+    }
     if (timing) {
       int bpc = 0, cus = 0;
       if (variant == 4)
@@ -466,20 +496,13 @@ std::vector<int> pfsp_expand_probe_t(const PfspInstance& in, const void* parents
 // loaded as the window. Returns every child's bound (parent order, children
 // k = depth..N-1), the children the kernel wrote (chunk order; lb < best, the leaves of
 // depth N-1 parents excluded), the leaves it counted and the incumbent after the launch.
-struct Lb1ProbeResult {
-  std::vector<int> bounds;
-  std::vector<uint8_t> children;
-  long long leaves = 0;
-  int best = 0;
-};
-
 template <int NJ, int M>
-Lb1ProbeResult pfsp_lb1_expand_probe_t(const PfspInstance& in, const void* parents, size_t n, int best, int device) {
+ExpandProbeResult pfsp_lb1_expand_probe_t(const PfspInstance& in, const void* parents, size_t n, int best, int device) {
   using Node = PfspNode<NJ>;
   using G = dev::PfspGeom<NJ, 1, M>;
   TTS_HIP_CHECK(hipSetDevice(device));
   const Node* ph = static_cast<const Node*>(parents);
-  Lb1ProbeResult res;
+  ExpandProbeResult res;
   std::vector<int> offsets(n + 1, 0);
   for (size_t i = 0; i < n; ++i) {
     if (ph[i].depth >= in.jobs) throw std::invalid_argument("lb1 expand probe: parents must have children");
@@ -825,12 +848,13 @@ decltype(auto) with_machine_bucket(int machines, F&& f) {
 std::unique_ptr<IEngine> make_pfsp_engine(const PfspInstance& in, int lb, const EngineConfig& cfg);
 std::vector<int> pfsp_gpu_bounds(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device);
 std::vector<int> pfsp_expand_probe(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device,
-                                   int variant, int reps = 0, std::vector<double>* timing = nullptr);
+                                   int variant, int reps = 0, std::vector<double>* timing = nullptr,
+                                   ExpandProbeResult* extra = nullptr);
 std::vector<double> pfsp_front_time(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
                                     const EngineConfig& cfg, int reps);
 // front-layout instances only (pfsp_front_ok), defined with the 20-job bucket (the
 // 50-job front bucket's in its own TU)
-Lb1ProbeResult pfsp_lb1_expand_probe(const PfspInstance& in, const void* parents, size_t n, int best, int device);
+ExpandProbeResult pfsp_lb1_expand_probe(const PfspInstance& in, const void* parents, size_t n, int best, int device);
 FrontProbeResult pfsp_front_probe(const PfspInstance& in, int lb, const void* nodes, size_t n, int best,
                                   const EngineConfig& cfg, unsigned cap, int split_rank = 0, int split_world = 1,
                                   size_t split_min = 0);
@@ -845,8 +869,9 @@ std::vector<double> pfsp_front_time_nj50(const PfspInstance& in, int lb, const v
   std::vector<int> pfsp_gpu_bounds_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
                                           int device);                                                \
   std::vector<int> pfsp_expand_probe_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
-                                            int device, int variant, int reps, std::vector<double>* timing); \
-  Lb1ProbeResult pfsp_lb1_expand_probe_nj##NJ(const PfspInstance& in, const void* parents, size_t n, int best, int device);
+                                            int device, int variant, int reps, std::vector<double>* timing, \
+                                            ExpandProbeResult* extra); \
+  ExpandProbeResult pfsp_lb1_expand_probe_nj##NJ(const PfspInstance& in, const void* parents, size_t n, int best, int device);
 TTS_PFSP_DECLARE_BUCKET(20)
 TTS_PFSP_DECLARE_BUCKET(50)
 TTS_PFSP_DECLARE_BUCKET(100)
@@ -878,14 +903,15 @@ TTS_PFSP_DECLARE_BUCKET(500)
     });                                                                                              \
   }                                                                                                  \
   std::vector<int> pfsp_expand_probe_nj##NJ(const PfspInstance& in, int lb, const void* parents, size_t n, int best, \
-                                            int device, int variant, int reps, std::vector<double>* timing) { \
+                                            int device, int variant, int reps, std::vector<double>* timing, \
+                                            ExpandProbeResult* extra) {                                     \
     if (lb != 2) throw std::invalid_argument("expand probe: LB2 only");                             \
     return with_machine_bucket(in.machines, [&](auto mm) {                                           \
       constexpr int M = decltype(mm)::value;                                                         \
-      return pfsp_expand_probe_t<NJ, M, 2>(in, parents, n, best, device, variant, reps, timing);    \
+      return pfsp_expand_probe_t<NJ, M, 2>(in, parents, n, best, device, variant, reps, timing, extra); \
     });                                                                                              \
   }                                                                                                  \
-  Lb1ProbeResult pfsp_lb1_expand_probe_nj##NJ(const PfspInstance& in, const void* parents, size_t n, int best, \
+  ExpandProbeResult pfsp_lb1_expand_probe_nj##NJ(const PfspInstance& in, const void* parents, size_t n, int best, \
                                               int device) {                                          \
     return with_machine_bucket(in.machines, [&](auto mm) {                                           \
       constexpr int M = decltype(mm)::value;                                                         \

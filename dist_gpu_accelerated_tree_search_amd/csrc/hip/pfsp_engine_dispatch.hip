@@ -24,17 +24,17 @@ std::vector<int> pfsp_gpu_bounds(const PfspInstance& in, int lb, const void* par
 }
 
 std::vector<int> pfsp_expand_probe(const PfspInstance& in, int lb, const void* parents, size_t n, int best, int device,
-                                   int variant, int reps, std::vector<double>* timing) {
+                                   int variant, int reps, std::vector<double>* timing, ExpandProbeResult* extra) {
   switch (pfsp_bucket(in.jobs)) {
-    case 20: return pfsp_expand_probe_nj20(in, lb, parents, n, best, device, variant, reps, timing);
-    case 50: return pfsp_expand_probe_nj50(in, lb, parents, n, best, device, variant, reps, timing);
-    case 100: return pfsp_expand_probe_nj100(in, lb, parents, n, best, device, variant, reps, timing);
-    case 200: return pfsp_expand_probe_nj200(in, lb, parents, n, best, device, variant, reps, timing);
-    default: return pfsp_expand_probe_nj500(in, lb, parents, n, best, device, variant, reps, timing);
+    case 20: return pfsp_expand_probe_nj20(in, lb, parents, n, best, device, variant, reps, timing, extra);
+    case 50: return pfsp_expand_probe_nj50(in, lb, parents, n, best, device, variant, reps, timing, extra);
+    case 100: return pfsp_expand_probe_nj100(in, lb, parents, n, best, device, variant, reps, timing, extra);
+    case 200: return pfsp_expand_probe_nj200(in, lb, parents, n, best, device, variant, reps, timing, extra);
+    default: return pfsp_expand_probe_nj500(in, lb, parents, n, best, device, variant, reps, timing, extra);
   }
 }
 
-Lb1ProbeResult pfsp_lb1_expand_probe(const PfspInstance& in, const void* parents, size_t n, int best, int device) {
+ExpandProbeResult pfsp_lb1_expand_probe(const PfspInstance& in, const void* parents, size_t n, int best, int device) {
   switch (pfsp_bucket(in.jobs)) {
     case 20: return pfsp_lb1_expand_probe_nj20(in, parents, n, best, device);
     case 50: return pfsp_lb1_expand_probe_nj50(in, parents, n, best, device);

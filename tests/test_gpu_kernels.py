@@ -126,3 +126,38 @@ def test_other_machine_counts_match_cpu(machines, lb):
     bk.best_known = ref.best  # -u 1 with the optimum: deterministic tree
     r1, g1 = solve_cpu(bk, ub=1), solve_gpu(bk, ub=1)
     assert (g1.tree, g1.sol, g1.best) == (r1.tree, r1.sol, r1.best)
+
+
+@pytest.mark.parametrize("inst,n", [(3, 300), (14, 300), (56, 120), (81, 40), (95, 16), (111, 6)])
+@pytest.mark.parametrize("variant", [1, 4])
+def test_lb2_expand_writes_the_surviving_children(inst, n, variant):
+    # what the LB2 expand iteration WRITES (phase C compaction), not only its bounds: the
+    # children with LB2 < best as a multiset of node bytes, the leaves counted, the incumbent
+    model = PfspModel(inst, 2)
+    if variant == 4 and (model.jobs + model.machines - 1) * max(model.native.p) >= 65536:
+        pytest.skip("packed walks need 16-bit walk values (lb2_pk_ok)")
+    rng = np.random.default_rng(inst * 3 + variant)
+    depths = rng.integers(0, model.jobs - 1, size=n)
+    depths[:2] = model.jobs - 1  # two parents of leaves
+    perms = np.stack([rng.permutation(model.jobs) for _ in range(n)])
+    nodes = nd.pfsp_pack(depths, perms, model.jobs)
+    cpu = model.child_bounds_cpu(nodes, INT_MAX)
+    best = int(np.median(cpu))
+    kids, leaves, inc, i = [], 0, best, 0
+    for d, q in zip(depths, perms):
+        for k in range(int(d), model.jobs):
+            b = int(cpu[i])
+            i += 1
+            if d + 1 == model.jobs:
+                leaves += 1
+                inc = min(inc, b)
+            elif b < best:
+                c = q.copy()
+                c[d], c[k] = c[k], c[d]
+                kids.append(bytes(nd.pfsp_pack([d + 1], [c], model.jobs)[0]))
+    r = ops.require_gpu(0).pfsp_expand_probe_out(model.jobs, model.machines, list(model.native.p), nodes, best, 0, variant)
+    got = sorted(bytes(x) for x in np.ascontiguousarray(r["children"]))
+    assert got == sorted(kids), (len(got), len(kids))
+    assert r["leaves"] == leaves and r["best"] == inc
+    below = cpu < best
+    assert np.array_equal(r["bounds"][below], cpu[below])
