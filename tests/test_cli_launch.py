@@ -97,3 +97,17 @@ def test_heuristic_ub_is_opt_in_and_recorded(tmp_path, monkeypatch, capsys):
     assert "Initial upper bound: inf" in capsys.readouterr().out
     rec = json.loads(out.read_text().splitlines()[-1])
     assert rec["initial_ub"] is None and rec["best"] == 1359
+
+
+def test_console_entry_point_resolves():
+    # pyproject's `tts` script is the CLI's main (pip install -e . puts it on PATH)
+    import importlib
+    import os
+
+    import tomli
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "pyproject.toml"), "rb") as f:
+        meta = tomli.load(f)
+    mod, fn = meta["project"]["scripts"]["tts"].split(":")
+    assert getattr(importlib.import_module(mod), fn) is cli.main
