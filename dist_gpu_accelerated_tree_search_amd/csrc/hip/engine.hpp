@@ -142,6 +142,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (const char* f = std::getenv("TTS_DEEP_P4")) pa.deep_per[1] = std::max(0, std::atoi(f));
     pa.wide_levels = cfg_.wide_levels;
     if (const char* f = std::getenv("TTS_WIDE_LEVELS")) pa.wide_levels = std::atoi(f);
+    pa.prune_fixed = 0;
     grid_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(max_chunks_, resident)));
     // the kernel's local DFS threshold only with a parent window of at least a resident
     // grid of chunks: a narrower window cannot take in what a local iteration leaves (up to
@@ -635,6 +636,8 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     // -u 0 (no incumbent yet): dive to the first leaves through a narrow window
     h_ctl_->slot[0].cap = (best == 0x7fffffff && cfg_.dive_window > 0) ? static_cast<unsigned>(cfg_.dive_window) : 0u;
     h_ctl_->slot[0].cpad = 0x7fffffffu;
+    // replicated iterations (a pending split) prune with this incumbent (pool_device.hpp prune_best)
+    h_ctl_->best0 = best;
     const bool armed = arm_world_ > 1;
     arm_world_ = 0;
     if (armed && n > cfg_.max_parents)
@@ -688,16 +691,21 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     // 6-iteration passes with a narrower parent window (plain launches: the
     // window is a kernel argument); identical on every rank
     const size_t win = std::max<size_t>(1, std::min(window, cfg_.max_parents));
-    if (phase_) {  // the passes below start from phase 0
-      normalize();
-      upload_ctl();
-    }
+    // the passes must be identical on every rank: no -u 0 dive cap in them (a dive reaches
+    // leaves, and an incumbent lowered in the middle of an iteration prunes differently
+    // from rank to rank); the rank's own search dives from its share afterwards
+    const unsigned dive_cap = h_ctl_->slot[0].cap;
+    h_ctl_->slot[0].cap = 0;
+    h_ctl_->best0 = h_ctl_->best.v;  // and prune every pass with the incumbent they start from
+    if (phase_) normalize();  // the passes below start from phase 0
+    upload_ctl();
     for (int p = 0; p < passes; ++p) {
       if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
       const size_t total = dev_total();
       if (total == 0 || total + 7 * buf_nodes_ > cap_) break;
       auto a = args_;
       a.pool.max_parents = static_cast<int>(win);
+      a.pool.prune_fixed = 1;
       a.pool.max_chunks = static_cast<int>((win + Traits::kParentsPerChunk - 1) / Traits::kParentsPerChunk);
       const int m = next_mirror_;
       next_mirror_ ^= 1;
@@ -712,6 +720,8 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     }
     if (h_ctl_->overflow) throw std::runtime_error("device pool overflow (ring too small)");
     normalize();
+    h_ctl_->slot[0].cap = h_ctl_->best.v == 0x7fffffff ? dive_cap : 0u;
+    if (world == 1) upload_ctl();
     if (world > 1) {
       // strided share of the device part, then of the host spill
       const size_t n = dev_stack();

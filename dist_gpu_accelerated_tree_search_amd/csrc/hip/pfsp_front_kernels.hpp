@@ -1299,7 +1299,7 @@ void pfsp_front_kernel(PfspFrontArgs<M, NJ> a, int t) {
     for (int i = 0; i < PTN; ++i)
       if (tid + i * kBlock < G::NJ * G::MS) pt[tid + i * kBlock] = ptv[i];
   }
-  const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int best = prune_best(pa, v);
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];

@@ -741,7 +741,7 @@ __device__ inline void pfsp_expand_lb2(const PfspArgs<NJ, M>& a, int t) {
   const unsigned long long t_entry = a.dbg_blk ? wall_clock64() : 0;
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
   if (v.B == 0 || v.overflow) return;
-  const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int best = prune_best(pa, v);
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];
@@ -1060,7 +1060,7 @@ __device__ inline void pfsp_expand_lb1(const PfspArgs<NJ, M>& a, int t) {
   const auto& pa = a.pool;
   const IterView v = pool_begin<Node, G::MAXCHUNKS>(pa, t, G::BP, sm.pool);
   if (v.B == 0 || v.overflow) return;
-  const int best = __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int best = prune_best(pa, v);
   Node* const bout = pa.buf[(t & 1) ^ 1];
   int* const cnt_out = pa.cnt[(t & 1) ^ 1];
   int* const lcnt_out = pa.lcnt[(t & 1) ^ 1];

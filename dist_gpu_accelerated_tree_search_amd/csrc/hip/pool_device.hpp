@@ -65,6 +65,10 @@ struct PoolCtl {
   int split_rank;
   int dive_shift;     // -u 0 dive: log2 of the cap's growth per iteration after the first leaf
   u64 split_min;
+  // Pruning threshold of replicated iterations (prune_best): the incumbent the solve began
+  // with (or the warm_split passes start from)
+  int best0;
+  int pad0;
   // nodes pushed and leaves counted inside subtrees a thread explored to the end (N-Queens
   // finishing: 64-bit counts, one accumulator line per 8th of the grid; the host folds them)
   struct alignas(128) XAcc {
@@ -124,6 +128,8 @@ struct PoolArgs {
   // wide multi-level iterations: a window of more than a narrow chunk's parents per
   // workgroup but at most one per thread is expanded this many levels deep (< 2: off)
   int wide_levels;
+  // 1: prune with ctl->best0, not the live incumbent (warm_split passes, identical on every rank)
+  int prune_fixed;
   // dynamic local DFS (front kernel): 3 DynCtl sets (null: off), the time budget of
   // one iteration in wall-clock ticks (100 MHz) and the queue slots (a multiple of 8)
   DynCtl* dyn;
@@ -472,6 +478,22 @@ __device__ inline IterView pool_begin(const PoolArgs<Node>& pa, int t, int BP, P
     }
   }
   return v;
+}
+
+// The incumbent an iteration prunes with. While a rank split is pending (or in the
+// warm_split passes: pa.prune_fixed) every rank must expand the replicated iterations identically, and the live
+// incumbent is not a rank-independent value there: a leaf found by one workgroup lowers it
+// for the workgroups that start later in the same kernel, and an incumbent received from a
+// peer between replays reaches the ranks at different iterations. Those iterations prune
+// with the incumbent the solve began with; leaves still lower ctl->best, which every
+// iteration after the split uses.
+template <class Node>
+__device__ inline int prune_best(const PoolArgs<Node>& pa, const IterView& v) {
+  // (the switch is uniform and known without a load: a kernel argument and the window view)
+#ifndef TTS_PRUNE_LIVE_AB  // (A/B builds only, scripts/build_variant.py: the live incumbent everywhere)
+  if (v.armed || pa.prune_fixed) return pa.ctl->best0;
+#endif
+  return __hip_atomic_load(&pa.ctl->best.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // (An XCD-aware chunk order — XCD x of the 8 taking a contiguous range of chunks, so a

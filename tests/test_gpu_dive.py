@@ -39,3 +39,48 @@ def test_dive_ta008_lb1d(monkeypatch):
     eng = m.make_engine("gpu", 0, EngineOptions(ring_bytes=4 << 30))
     r = solve_engine(m, eng, ub=0)
     assert r.best == 1206 and r.tree >= 113458723
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_warm_split_from_inf_is_rank_independent(world, monkeypatch):
+    # warm_split passes run without the dive cap and prune with the incumbent they start
+    # from (pool_device.hpp prune_best): every rank builds the same pool, then each share
+    # dives from +inf on its own; the best share finds the optimum
+    monkeypatch.delenv("TTS_DIVE", raising=False)
+    m = PfspModel(14, 1)
+    opts = EngineOptions(ring_bytes=1 << 30)
+
+    def pool(rank, w):
+        e = m.make_engine("gpu", 0, opts)
+        e.begin(m.root(), INT_MAX)
+        n = e.warm_split(rank, w, 1024, 1)
+        return e, e.pop(n)
+
+    _, full = pool(0, 1)
+    bests, tree = [], 0
+    for r in range(world):
+        e, nodes = pool(r, world)
+        assert (nodes == full[r::world]).all()
+        e.push(nodes)
+        e.run()
+        st = e.stats()
+        bests.append(st["best"])
+        tree += st["tree"]
+    assert min(bests) == 1377 and tree >= GOLD14[0] // 2
+
+
+def test_warm_split_exhausts_small_tree_from_inf(monkeypatch):
+    # a warm-up target beyond the whole tree: the passes reach the leaves, so the pruning
+    # threshold must not move inside them for every rank to count the same tree
+    monkeypatch.delenv("TTS_DIVE", raising=False)
+    m = PfspModel.synthetic(6, 4, 11, lb=1)
+    got = []
+    for r, w in ((0, 1), (0, 2), (1, 2)):
+        e = m.make_engine("gpu", 0, EngineOptions(ring_bytes=1 << 26, max_parents=1 << 14))
+        e.begin(m.root(), INT_MAX)
+        n = e.warm_split(r, w, 1 << 20, 2)
+        st = e.stats()
+        got.append((n, st["best"], st["tree"], st["sol"]))
+    assert [g[0] for g in got] == [0, 0, 0]
+    assert got[0][1] == got[1][1] == got[2][1] == solve_cpu(m, ub=0).best
+    assert got[1][2:] == got[0][2:] and got[0][2] > 0 and got[2][2:] == (0, 0)
