@@ -38,14 +38,27 @@ struct QueensArgs {
 
 constexpr int kQueensFinishMax = 9;  // columns left at most in a finished subtree
 
+// Nodes per wave in the LDS stack of the wave-cooperative subtree finishing (3 masks each)
+#ifndef TTS_QSTACK
+#define TTS_QSTACK 768
+#endif
+constexpr int kQStack = TTS_QSTACK;
+
 struct QueensSmem {
   static constexpr int BP = kBlock;
   static constexpr int MAXCH = BP * 32;
   static constexpr int MAXCHUNKS = 4096;
-  QueensNode node[BP];
-  uint32_t avail[BP];
-  int off[BP];
-  uint8_t map[MAXCH];
+  // the level-by-level arrays of the chunk loop and the finishing stacks (after the
+  // loop's last barrier) share their LDS
+  union {
+    struct {
+      QueensNode node[BP];
+      uint32_t avail[BP];
+      int off[BP];
+      uint8_t map[MAXCH];
+    };
+    uint32_t st[kBlock / kWave][3][kQStack];  // per wave: cols, diag, anti
+  };
   int scan[kBlock / kWave];
   int red[kBlock / kWave];
   u64 fin[kBlock / kWave][2];
@@ -107,6 +120,76 @@ __device__ inline void queens_dfs(uint32_t cols, uint32_t diag, uint32_t anti, i
       queens_dfs<L + 1>(cols | bit, (diag | bit) << 1, (anti | bit) >> 1, depth + 1, a, tree, sol);
     }
   }
+}
+
+// Wave-cooperative subtree finishing. The wave's finishing parents go on an LDS stack
+// (three mask arrays per wave, kQStack nodes); each pass pops up to 64 nodes from the top,
+// one per lane, counts their safe children with the pool's rules (tree; sol in the last
+// column) and pushes the children of nodes above the last column back on top, at offsets
+// from a ballot prefix sum. Every lane bounds a node in every pass: no lane idles while
+// another walks a longer subtree, which is what the register walk above pays for (a wave
+// executes the union of its lanes' walks). A node whose children would not fit the stack
+// is walked in registers by its lane (queens_dfs, same counts).
+__device__ inline void queens_finish_wave(uint32_t (*st)[kQStack], int sp, const QueensArgs& a, u64& tree,
+                                          u64& sol) {
+  const int lane = static_cast<int>(threadIdx.x) & (kWave - 1);
+  uint32_t t32 = 0, s32 = 0;
+  while (sp > 0) {
+    const int n = min(sp, kWave);
+    const int base = sp - n;
+    uint32_t cols = 0, diag = 0, anti = 0, av = 0;
+    int depth = 0;
+    if (lane < n) {
+      cols = st[0][base + lane];
+      diag = st[1][base + lane];
+      anti = st[2][base + lane];
+      depth = __popc(cols);
+      av = queens_free_rows(QueensNode{cols, diag, anti, static_cast<uint32_t>(depth)}, a.full, a.G);
+    }
+    const int c = __popc(av);
+    const bool last = depth + 1 == a.N;
+    int cpush = last ? 0 : c;
+    // exclusive wave prefix of the pushed counts (at most 32: six ballots)
+    int off = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const u64 bal = __ballot((cpush >> k) & 1);
+      off += static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u)))
+             << k;
+      total += __popcll(bal) << k;
+    }
+    const int room = kQStack - base;
+    bool walk = false;
+    if (total > room) {
+      // the lanes from the first one whose children do not fit walk their nodes in registers
+      const bool fits = cpush == 0 || off + cpush <= room;
+      const u64 nf = __ballot(!fits);
+      total = __builtin_amdgcn_readlane(off, static_cast<int>(__builtin_ctzll(nf)));
+      walk = !fits;
+    }
+    if (walk) {
+      queens_dfs<0>(cols, diag, anti, depth, a, tree, sol);
+      cpush = 0;
+    } else {
+      t32 += static_cast<uint32_t>(c);
+      if (last) s32 += static_cast<uint32_t>(c);
+    }
+    uint32_t m = cpush ? av : 0u;
+    int p = base + off;
+    while (m) {
+      const uint32_t bit = m & (0u - m);
+      m ^= bit;
+      st[0][p] = cols | bit;
+      st[1][p] = (diag | bit) << 1;
+      st[2][p] = (anti | bit) >> 1;
+      ++p;
+    }
+    __builtin_amdgcn_wave_barrier();
+    sp = base + total;
+  }
+  tree += t32;
+  sol += s32;
 }
 
 // Position of the r-th (0-based) set bit of x (r < popcount(x)).
@@ -187,6 +270,9 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
     // workgroups catch up instead of trailing (N=17 170 -> 174 G nodes/s,
     // profiles/r5/queens_prio_ab.txt; the same age-priority effect as front_local's)
     int k = 0;
+#ifndef TTS_QUEENS_REGWALK_AB
+    uint32_t (*const st)[kQStack] = sm.st[tid / kWave];
+#endif
     for (int ch = blockIdx.x; ch < v.nchunks; ch += gridDim.x) {
       if (k == 0) __builtin_amdgcn_s_setprio(3);
       else if (k == 1) __builtin_amdgcn_s_setprio(2);
@@ -194,11 +280,28 @@ __global__ __launch_bounds__(kBlock) void queens_expand_kernel(QueensArgs a, int
       else __builtin_amdgcn_s_setprio(0);
       ++k;
       const u64 gi = static_cast<u64>(ch) * S::BP + tid;
+      QueensNode nd{0, 0, 0, 0};
+      bool fin = false;
       if (gi < v.B) {
-        const QueensNode nd = *pool_parent<QueensNode, S::MAXCH, S::MAXCHUNKS>(pa, v, t, gi, sm.pool);
+        nd = *pool_parent<QueensNode, S::MAXCH, S::MAXCHUNKS>(pa, v, t, gi, sm.pool);
         const int d = static_cast<int>(nd.depth);
-        if (d < a.N && d >= fin_from) queens_dfs<0>(nd.cols, nd.diag, nd.anti, d, a, ftree, fsol);
+        fin = d < a.N && d >= fin_from;
       }
+#ifdef TTS_QUEENS_REGWALK_AB  // (A/B builds only: the per-lane register walk)
+      if (fin) queens_dfs<0>(nd.cols, nd.diag, nd.anti, static_cast<int>(nd.depth), a, ftree, fsol);
+#else
+      // this wave's finishing parents start its stack (at most 64 <= kQStack)
+      const u64 bal = __ballot(fin);
+      if (fin) {
+        const int pos = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u)));
+        st[0][pos] = nd.cols;
+        st[1][pos] = nd.diag;
+        st[2][pos] = nd.anti;
+      }
+      __builtin_amdgcn_wave_barrier();
+      queens_finish_wave(st, __popcll(bal), a, ftree, fsol);
+#endif
     }
     // one pair of 64-bit adds per workgroup, on the line of its 8th of the grid
 #pragma unroll
