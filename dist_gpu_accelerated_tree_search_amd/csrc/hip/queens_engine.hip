@@ -45,8 +45,11 @@ static dev::QueensArgs queens_args(int N, int G) {
   a.G = G;
   a.full = N == 32 ? 0xffffffffu : ((1u << N) - 1u);
   // subtree finishing: parents with at most finish_k columns left (TTS_QUEENS_FINISH
-  // overrides; 0 = level-by-level to the bottom)
-  a.finish_k = 7;
+  // overrides; 0 = level-by-level to the bottom). The wave-cooperative finishing is
+  // fastest from 9 columns left (N=17: 6 / 7 / 8 / 9 / 10 / 11 / 12 columns 48 / 29 / 24 /
+  // 21 / 25 / 37 / 138 ms; deeper subtrees overflow the LDS stacks into the register walk,
+  // profiles/r6/queens/finish_depth_ab.txt)
+  a.finish_k = 9;
   if (const char* f = std::getenv("TTS_QUEENS_FINISH")) a.finish_k = std::atoi(f);
   a.finish_k = std::max(0, std::min(a.finish_k, dev::kQueensFinishMax));
   return a;

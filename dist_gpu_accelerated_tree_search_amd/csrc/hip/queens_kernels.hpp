@@ -36,11 +36,14 @@ struct QueensArgs {
   int nparents;
 };
 
-constexpr int kQueensFinishMax = 9;  // columns left at most in a finished subtree
+constexpr int kQueensFinishMax = 12;  // columns left at most in a finished subtree
 
-// Nodes per wave in the LDS stack of the wave-cooperative subtree finishing (3 masks each)
+// Nodes per wave in the LDS stack of the wave-cooperative subtree finishing (3 masks each).
+// 448 is the largest that keeps 4 workgroups per CU (N=17 finishing from 7 columns left:
+// 768 / 448 / 320 / 256 / 192 nodes 37 / 32 / 34 / 32 / 37 ms; from 9 columns: 448 / 640
+// nodes 21 / 22 ms; profiles/r6/queens/)
 #ifndef TTS_QSTACK
-#define TTS_QSTACK 768
+#define TTS_QSTACK 448
 #endif
 constexpr int kQStack = TTS_QSTACK;
 
@@ -149,10 +152,12 @@ __device__ inline void queens_finish_wave(uint32_t (*st)[kQStack], int sp, const
     const int c = __popc(av);
     const bool last = depth + 1 == a.N;
     int cpush = last ? 0 : c;
-    // exclusive wave prefix of the pushed counts (at most 32: six ballots)
+    // exclusive wave prefix of the pushed counts: a stacked node has at most
+    // kQueensFinishMax columns left, so at most 15 children (four ballots)
+    static_assert(kQueensFinishMax < 16, "pushed counts must fit four bits");
     int off = 0, total = 0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < 4; ++k) {
       const u64 bal = __ballot((cpush >> k) & 1);
       off += static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
                                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u)))

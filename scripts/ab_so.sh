@@ -20,4 +20,4 @@ except Exception:
     print('\n'.join('$v run $r: '+l for l in lines))"
   done
 done
-cp "build/ab/base/$(basename "$mod")" "$mod"
+cp "build/ab/${vars%%,*}/$(basename "$mod")" "$mod"

@@ -13,7 +13,7 @@ OPTS = EngineOptions(max_parents=1 << 20, ring_bytes=1 << 30)
 
 @pytest.mark.parametrize("k", [0, 1, 2, 5, 7, 9, 20])
 def test_finishing_depths_keep_the_tree(k, monkeypatch):
-    monkeypatch.setenv("TTS_QUEENS_FINISH", str(k))  # 20: clamped to the deepest template (9)
+    monkeypatch.setenv("TTS_QUEENS_FINISH", str(k))  # 20: clamped to the deepest template (12)
     for N, gold in GOLD.items():
         m = QueensModel(N)
         eng = m.make_engine("gpu", 0, OPTS)
