@@ -39,7 +39,7 @@ struct QueensArgs {
 constexpr int kQueensFinishMax = 12;  // columns left at most in a finished subtree
 
 // Nodes per wave in the LDS stack of the wave-cooperative subtree finishing (3 masks each).
-// 448 is the largest that keeps 4 workgroups per CU (N=17 finishing from 7 columns left:
+// 448 keeps 5 workgroups per CU with the 2048-chunk window (4 with 4096 chunks) (N=17 finishing from 7 columns left:
 // 768 / 448 / 320 / 256 / 192 nodes 37 / 32 / 34 / 32 / 37 ms; from 9 columns: 448 / 640
 // nodes 21 / 22 ms; profiles/r6/queens/)
 #ifndef TTS_QSTACK
@@ -50,7 +50,12 @@ constexpr int kQStack = TTS_QSTACK;
 struct QueensSmem {
   static constexpr int BP = kBlock;
   static constexpr int MAXCH = BP * 32;
-  static constexpr int MAXCHUNKS = 4096;
+// (2048 chunks = a 2^19-parent window: the 8 KB of chunk prefix it saves give a fifth
+// workgroup per CU, N=17 21 -> 20 ms)
+#ifndef TTS_QMAXCHUNKS
+#define TTS_QMAXCHUNKS 2048
+#endif
+  static constexpr int MAXCHUNKS = TTS_QMAXCHUNKS;
   // the level-by-level arrays of the chunk loop and the finishing stacks (after the
   // loop's last barrier) share their LDS
   union {
@@ -151,6 +156,8 @@ __device__ inline void queens_finish_wave(uint32_t (*st)[kQStack], int sp, const
     }
     const int c = __popc(av);
     const bool last = depth + 1 == a.N;
+    // (counting the next-to-last column's boards in the parent's lane instead of pushing
+    // it measured slower: N=17 21 -> 25 ms, profiles/r6/queens/finish_depth_ab.txt)
     int cpush = last ? 0 : c;
     // exclusive wave prefix of the pushed counts: a stacked node has at most
     // kQueensFinishMax columns left, so at most 15 children (four ballots)
