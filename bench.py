@@ -271,9 +271,11 @@ def run_queens_extra(a, comm, device: int, N: int) -> dict:
     from dist_gpu_accelerated_tree_search_amd.parallel.runtime import DistConfig
 
     model = QueensModel(N, 1)
-    # two engines per GPU with the solve split between them in the graph: N=17 74 -> 48 ms
-    # on one MI355X (profiles/r3/queens/streams_probe.txt)
-    opts = EngineOptions(max_parents=1 << 20, ring_bytes=8 << 30, streams=2, stream_split=512) \
+    # engines per GPU with the solve split between them in the graph: N=17 74 -> 48 ms with
+    # two (profiles/r3/queens/streams_probe.txt); with the wave-stack finishing and transfer
+    # streams created on first use (each engine's compute stream on its own hardware queue)
+    # three: 20.4 -> 18.2 ms (profiles/r6/queens/lazy_xfer_ab.txt)
+    opts = EngineOptions(max_parents=1 << 19, ring_bytes=8 << 30, streams=3, stream_split=512) \
         if a.backend == "gpu" else EngineOptions(streams=2, stream_split=8)
     t_setup = time.perf_counter()
     engine, solver = _agreed_setup(comm, f"N-Queens N={N}", lambda: _make_solver(

@@ -104,7 +104,9 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_comp_, hipEventDisableTiming));
     TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_xfer_, hipEventDisableTiming));
     TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_ahead_, hipEventDisableTiming));
+#ifdef TTS_EAGER_XFER_AB  // (A/B builds only: the transfer stream created with the engine)
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&xfer_, hipStreamNonBlocking));
+#endif
     std::memset(h_ctl_, 0, sizeof(dev::PoolCtl));
     h_ctl_->best.v = 0x7fffffff;
     h_ctl_->dive_shift = cfg_.dive_shift;
@@ -279,7 +281,17 @@ class DeviceEngine final : public IEngine, public DeviceResource {
 
   size_t node_bytes() const override { return sizeof(Node); }
   uintptr_t stream() const override { return reinterpret_cast<uintptr_t>(stream_); }
-  uintptr_t transfer_stream() const override { return reinterpret_cast<uintptr_t>(xfer_); }
+  uintptr_t transfer_stream() const override { return reinterpret_cast<uintptr_t>(xs()); }
+  // The transfer stream is created on first use: HIP maps a process's streams onto its
+  // hardware queues (GPU_MAX_HW_QUEUES, 4) in creation order, so engines that never
+  // transfer (one GPU) leave the queues to the compute streams of the other engines
+  hipStream_t xs() const {
+    if (!xfer_) {
+      TTS_HIP_CHECK(hipSetDevice(cfg_.device));
+      TTS_HIP_CHECK(hipStreamCreateWithFlags(&xfer_, hipStreamNonBlocking));
+    }
+    return xfer_;
+  }
   void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
   void set_trace(bool on) override {
     trace_clear();
@@ -289,7 +301,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     flush_load();
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
-    TTS_HIP_CHECK(hipStreamSynchronize(xfer_));
+    if (xfer_) TTS_HIP_CHECK(hipStreamSynchronize(xfer_));
     std::vector<double> out;
     if (trace_rec_.empty()) return out;
     const hipEvent_t ref = trace_rec_.front().a;
@@ -318,7 +330,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     TTS_HIP_CHECK(hipSetDevice(cfg_.device));
     flush_load();
     TTS_HIP_CHECK(hipStreamSynchronize(stream_));
-    TTS_HIP_CHECK(hipStreamSynchronize(xfer_));
+    if (xfer_) TTS_HIP_CHECK(hipStreamSynchronize(xfer_));
   }
   int device() const override { return cfg_.device; }
   int grid() const { return grid_; }
@@ -371,10 +383,10 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     const size_t n = std::min(max_n, dev_stack());
     if (n == 0) return 0;
     // the staging buffer may still be read by the previous send on the transfer stream
-    order(xfer_, stream_);
+    order(xs(), stream_);
     ring_read_bottom(static_cast<Node*>(dst), n, hipMemcpyDeviceToDevice);
     upload_ctl();
-    order(stream_, xfer_);  // the send waits for the copy
+    order(stream_, xs());  // the send waits for the copy
     ++stats_.exports;
     return n;
   }
@@ -388,10 +400,10 @@ class DeviceEngine final : public IEngine, public DeviceResource {
       // make room on the device: the ring bottom goes to the pinned spill
       spill_bottom(dev_stack() + reserved_ + n - cap_ / 2);
     }
-    order(xfer_, stream_);  // the receive has landed
+    order(xs(), stream_);  // the receive has landed
     ring_write_top(static_cast<const Node*>(src), n, hipMemcpyDeviceToDevice);
     upload_ctl();
-    order(stream_, xfer_);  // the next receive into the buffer waits for this copy
+    order(stream_, xs());  // the next receive into the buffer waits for this copy
     ++stats_.imports;
   }
 
@@ -852,14 +864,14 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     if (exportable_ahead() < n) return false;
     const size_t start = (h_ctl_->bot + export_pending_) & (cap_ - 1);
     const size_t first = std::min(n, cap_ - start);
-    TTS_HIP_CHECK(hipMemcpyAsync(dst, d_ring_ + start, first * sizeof(Node), hipMemcpyDeviceToDevice, xfer_));
+    TTS_HIP_CHECK(hipMemcpyAsync(dst, d_ring_ + start, first * sizeof(Node), hipMemcpyDeviceToDevice, xs()));
     if (first < n)
-      TTS_HIP_CHECK(hipMemcpyAsync(dst + first, d_ring_, (n - first) * sizeof(Node), hipMemcpyDeviceToDevice, xfer_));
+      TTS_HIP_CHECK(hipMemcpyAsync(dst + first, d_ring_, (n - first) * sizeof(Node), hipMemcpyDeviceToDevice, xs()));
     export_pending_ += n;
     // the ring span is handed back to the compute stream only after this copy
     // (commit_export makes the stream wait for it: a replay that wraps around the ring
     // must not overwrite nodes still being copied out behind a slow transfer queue)
-    TTS_HIP_CHECK(hipEventRecord(ev_ahead_, xfer_));
+    TTS_HIP_CHECK(hipEventRecord(ev_ahead_, xs()));
     ahead_copy_ = true;
     ++stats_.exports;
     ++stats_.overlapped_exports;
@@ -1064,17 +1076,17 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     flush_load();
     n = std::min(n, dev_stack());
     if (n == 0) return;
-    order(stream_, xfer_);  // the nodes were written by earlier replays
+    order(stream_, xs());  // the nodes were written by earlier replays
     const size_t start = h_ctl_->bot & (cap_ - 1);
     const size_t first = std::min(n, cap_ - start);
     auto reserve = [&](hipEvent_t ev, size_t k) {
       resv_.emplace_back(ev, k);
       reserved_ += k;
     };
-    const hipEvent_t tr = trace_ ? trace_mark(xfer_) : nullptr;
-    spill_.push_from_device(d_ring_ + start, first, xfer_, reserve);
-    if (first < n) spill_.push_from_device(d_ring_, n - first, xfer_, reserve);
-    if (tr) trace_rec_.push_back({1, tr, trace_mark(xfer_)});
+    const hipEvent_t tr = trace_ ? trace_mark(xs()) : nullptr;
+    spill_.push_from_device(d_ring_ + start, first, xs(), reserve);
+    if (first < n) spill_.push_from_device(d_ring_, n - first, xs(), reserve);
+    if (tr) trace_rec_.push_back({1, tr, trace_mark(xs())});
     h_ctl_->bot = (h_ctl_->bot + n) & (cap_ - 1);
     h_ctl_->slot[0].stack -= n;
     stats_.spilled += n;
@@ -1095,10 +1107,10 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     const size_t start = h_ctl_->bot & (cap_ - 1);
     const size_t first = std::min(n, cap_ - start);
     auto reserve = [&](hipEvent_t ev, size_t k) { ahead_.emplace_back(ev, k); };
-    const hipEvent_t tr = trace_ ? trace_mark(xfer_) : nullptr;
-    spill_.push_from_device(d_ring_ + start, first, xfer_, reserve);
-    if (first < n) spill_.push_from_device(d_ring_, n - first, xfer_, reserve);
-    if (tr) trace_rec_.push_back({1, tr, trace_mark(xfer_)});
+    const hipEvent_t tr = trace_ ? trace_mark(xs()) : nullptr;
+    spill_.push_from_device(d_ring_ + start, first, xs(), reserve);
+    if (first < n) spill_.push_from_device(d_ring_, n - first, xs(), reserve);
+    if (tr) trace_rec_.push_back({1, tr, trace_mark(xs())});
     ahead_n_ = n;
   }
   void commit_spill_ahead() {
@@ -1132,9 +1144,9 @@ class DeviceEngine final : public IEngine, public DeviceResource {
     const size_t k = std::min({want, spill_.top_count(), limit - used, b0 ? b0 : cap_});
     if (k == 0) return false;
     Node* dst = d_ring_ + ((b0 + cap_ - k) & (cap_ - 1));
-    const hipEvent_t tr = trace_ ? trace_mark(xfer_) : nullptr;
-    if (spill_.pop_to_device(dst, k, xfer_, &refill_ev_) != k) throw std::logic_error("pinned spill: short refill");
-    if (tr) trace_rec_.push_back({2, tr, trace_mark(xfer_)});
+    const hipEvent_t tr = trace_ ? trace_mark(xs()) : nullptr;
+    if (spill_.pop_to_device(dst, k, xs(), &refill_ev_) != k) throw std::logic_error("pinned spill: short refill");
+    if (tr) trace_rec_.push_back({2, tr, trace_mark(xs())});
     refill_n_ = k;
     reserved_ += k;
     return true;
@@ -1270,7 +1282,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   hipEvent_t graph_done_[2] = {nullptr, nullptr};
   hipEvent_t up_done_ = nullptr;
   hipEvent_t ev_comp_ = nullptr, ev_xfer_ = nullptr;  // stream ordering (order())
-  hipStream_t xfer_ = nullptr;                         // spills, refills, work-sharing sends/receives
+  mutable hipStream_t xfer_ = nullptr;                 // spills, refills, work-sharing sends/receives (xs())
   // replay / copy timeline (set_trace): timing events, freed by trace_clear
   struct TraceRec {
     int kind;
@@ -1287,7 +1299,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   void trace_clear() {
     if (!trace_rec_.empty()) {
       (void)hipStreamSynchronize(stream_);
-      (void)hipStreamSynchronize(xfer_);
+      if (xfer_) (void)hipStreamSynchronize(xfer_);
     }
     for (auto& r : trace_rec_) {
       (void)hipEventDestroy(r.a);

@@ -15,8 +15,10 @@ from dist_gpu_accelerated_tree_search_amd.search import solve_engine  # noqa: E4
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 17
 GOLD = {17: (8017021931, 95815104), 16: (1141190302, 14772512)}
 m = QueensModel(N, 1)
-for streams, split, mp in ((1, 0, 1 << 19), (2, 512, 1 << 19), (2, 128, 1 << 19), (2, 2048, 1 << 19), (3, 512, 1 << 19),
-                           (4, 512, 1 << 19), (2, 512, 1 << 18), (1, 0, 1 << 18)):
+CONFIGS = ((2, 512, 1 << 19), (3, 512, 1 << 19), (4, 512, 1 << 19), (4, 512, 1 << 18), (8, 512, 1 << 17))
+if len(sys.argv) > 2:
+    CONFIGS = tuple(tuple(int(x) for x in c.split(":")) for c in sys.argv[2].split(","))
+for streams, split, mp in CONFIGS:
     eng = m.make_engine("gpu", 0, EngineOptions(max_parents=mp, ring_bytes=8 << 30, streams=streams,
                                                 stream_split=split))
     solve_engine(m, eng)
