@@ -28,6 +28,7 @@
 #include <memory>
 #include <thread>
 #include <type_traits>
+#include <mutex>
 #include <vector>
 
 #include "../core/engine_api.hpp"
@@ -285,11 +286,13 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   // The transfer stream is created on first use: HIP maps a process's streams onto its
   // hardware queues (GPU_MAX_HW_QUEUES, 4) in creation order, so engines that never
   // transfer (one GPU) leave the queues to the compute streams of the other engines
+  // (once: the round loop may ask for it from another thread than the engine's)
   hipStream_t xs() const {
-    if (!xfer_) {
+    std::call_once(xfer_once_, [this] {
+      if (xfer_) return;
       TTS_HIP_CHECK(hipSetDevice(cfg_.device));
       TTS_HIP_CHECK(hipStreamCreateWithFlags(&xfer_, hipStreamNonBlocking));
-    }
+    });
     return xfer_;
   }
   void set_progress_hook(ProgressHook hook) override { hook_ = std::move(hook); }
@@ -1282,6 +1285,7 @@ class DeviceEngine final : public IEngine, public DeviceResource {
   hipEvent_t graph_done_[2] = {nullptr, nullptr};
   hipEvent_t up_done_ = nullptr;
   hipEvent_t ev_comp_ = nullptr, ev_xfer_ = nullptr;  // stream ordering (order())
+  mutable std::once_flag xfer_once_;
   mutable hipStream_t xfer_ = nullptr;                 // spills, refills, work-sharing sends/receives (xs())
   // replay / copy timeline (set_trace): timing events, freed by trace_clear
   struct TraceRec {
