@@ -282,10 +282,12 @@ def _nqueens_parser(cls=argparse.ArgumentParser) -> argparse.ArgumentParser:
     ap.add_argument("-m", type=int, default=25)
     ap.add_argument("-M", type=int, default=50000)
     ap.add_argument("-D", type=int, default=1)
-    ap.add_argument("--max-parents", type=int, default=1 << 20)
+    ap.add_argument("--max-parents", type=int, default=1 << 19)
     # engines per GPU, the solve split in the graph between them: N=17 74 -> 48 ms on one
-    # MI355X with 2 (profiles/r3/queens/streams_probe.txt)
-    ap.add_argument("--streams", type=int, default=2)
+    # MI355X with 2 (profiles/r3/queens/streams_probe.txt); with the wave-stack finishing
+    # and each engine's compute stream on its own hardware queue, 3: 20.4 -> 18.2 ms
+    # (profiles/r6/queens/lazy_xfer_ab.txt; the kernel's window is at most 2^19 parents)
+    ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--stream-split", type=int, default=512)
     return ap
 
