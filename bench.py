@@ -106,6 +106,9 @@ def main() -> int:
     ap.add_argument("--extra-ring-gb", type=float, default=64.0)
     ap.add_argument("--extra-streams", type=int, default=3,
                     help="engines per GPU for the extras (csrc/core/multi_engine.hpp; 1 = one engine)")
+    ap.add_argument("--extra-streams-lb2", type=int, default=4,
+                    help="engines per GPU for the LB2 extra (ta056 0.177 -> 0.179 G nodes/s with 4; "
+                         "ta021 keeps 3: profiles/r6/extras_streams_3_vs_4.txt)")
     ap.add_argument("--extra-max-parents", type=int, default=1 << 19)
     a = ap.parse_args()
     out = Emitter()  # before anything can write to stdout
@@ -311,7 +314,8 @@ def run_solve_extra(a, comm, device: int, inst: int, lb: int, time_limit: float)
 
     model = PfspModel(inst, lb)
     # big trees: several engines per GPU fill it better than one (profiles/r3/streams*.txt)
-    opts = EngineOptions(ring_bytes=int(a.extra_ring_gb * (1 << 30)), streams=max(1, a.extra_streams),
+    streams = max(1, a.extra_streams_lb2 if lb == 2 else a.extra_streams)
+    opts = EngineOptions(ring_bytes=int(a.extra_ring_gb * (1 << 30)), streams=streams,
                          max_parents=a.extra_max_parents)
     t_setup = time.perf_counter()
     cfg = DistConfig(init_per_rank=a.init_per_rank, ws=not a.no_ws, L=not a.no_ws, time_limit_s=time_limit)
@@ -327,7 +331,7 @@ def run_solve_extra(a, comm, device: int, inst: int, lb: int, time_limit: float)
     d = {"config": name, "n_gpus": comm.world, "seconds": dt, "tree": r.tree, "sol": r.sol, "makespan": r.best,
          "nodes_per_s": r.tree / dt, "complete": bool(r.extra.get("complete", True)),
          "rounds": r.extra.get("rounds"), "per_rank_tree": [w.tree for w in r.workers],
-         "engine_setup_s": t_setup, "engines_per_gpu": max(1, a.extra_streams), "max_parents": opts.max_parents,
+         "engine_setup_s": t_setup, "engines_per_gpu": streams, "max_parents": opts.max_parents,
          # where the ranks' time went (the round loop's clocks): idle without work, load
          # balancing (plan + transfers), termination checks; rounds that overlapped replays
          "per_rank_t_idle": [round(w.t_idle, 4) for w in r.workers],
